@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""All-pairs route tables on MI355X -- the BASELINE.json metric.
+
+Workload (BASELINE.json configs[2], the metric's config): the k=48 fat-tree
+(2,880 switches, 110,592 directed links, 27,648 hosts).  One step computes the
+reference's default route (``TopologyDB.find_route``, LIFO search of
+``sdnmpi/util/topology_db.py:59-84``) for EVERY host pair as per-source
+tables: one tree (parent + out-port per switch) for each of the 1,152
+host-bearing edge switches = 27,648^2 = 7.64e8 host-pair routes.  Inputs
+(CSR, source list) are resident in HBM before the timed region; outputs stay
+in HBM.
+
+Multi-GPU (torchrun, one rank per GPU, RCCL): the sources are split into
+contiguous blocks, each rank builds its block, and one all-gather assembles
+the full [sources][V] tables on every rank (the exchange step of the north
+star); fixed total work -> "scaling": "strong".
+
+The JSON line also carries
+  roofline      algorithmic bytes of the DFS kernel per launch
+                (B_src = 4(V+1) + 4E + 4(V-1) + 8V per source)
+                / its mean duration from HIP events on its stream, vs 8 TB/s;
+  cpu_baseline  the oracle's per-source C restatement on the host cores
+                (rank 0, N = 1), same workload;
+  cpu_reference_path  the per-pair Python restatement of find_route (the
+                reference's own algorithm shape) on a bounded pair sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sdn-mpi-router_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from sdnmpi_amd import _native  # noqa: E402
+from sdnmpi_amd import topologies as T  # noqa: E402
+
+METRIC = "all-pairs routes/sec + % HBM roofline, k=48 fat-tree, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--fabric", default="fat_tree:48")
+    ap.add_argument("--mode", choices=["dfs", "shortest"], default="dfs")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget-s", type=float, default=20.0,
+                    help="bound on the CPU baseline's work")
+    return ap.parse_args()
+
+
+def algorithmic_bytes_per_source(V, E, mode):
+    if mode == "dfs":
+        # row_ptr + col (CSR read per source) + tree-edge port reads + parent/port writes
+        return 4 * (V + 1) + 4 * E + 4 * (V - 1) + 8 * V
+    # shortest: CSR read + dist (2 B) + nh/nh_port (8 B) writes per destination
+    return 4 * (V + 1) + 4 * E + 10 * V
+
+
+def cpu_baseline(fabric, csr, srcs, hosts_per_src, H, budget_s):
+    from oracle import oracle as O
+    threads = max(1, min(16, os.cpu_count() or 1))
+    # calibrate on a few sources, then run a bounded sample
+    probe = srcs[: max(1, min(len(srcs), threads))]
+    t0 = time.perf_counter()
+    O.dfs_tables(csr, probe, with_hops=False, nthreads=threads)
+    per_src = (time.perf_counter() - t0) / len(probe) * threads
+    n = int(min(len(srcs), max(threads, budget_s * threads / max(per_src, 1e-9))))
+    sample = srcs[:n]
+    t0 = time.perf_counter()
+    O.dfs_tables(csr, sample, with_hops=False, nthreads=threads)
+    dt = time.perf_counter() - t0
+    routes = float(hosts_per_src[:n].sum()) * H
+    out = {"value": routes / dt, "unit": "routes/s", "cores": threads, "kind": "port",
+           "sample": "oracle/sdnroute_oracle.c per-source DFS trees (same algorithm, "
+                     "pthreads) for %d of %d sources, %.2f s" % (n, len(srcs), dt)}
+    # the reference's own shape: one Python stack search per host pair
+    db = _DictDB()
+    fabric.populate(db)
+    macs = fabric.host_macs()
+    rng = np.random.default_rng(0)
+    t0 = time.perf_counter()
+    k = 0
+    while time.perf_counter() - t0 < min(5.0, budget_s / 4):
+        a, b = rng.integers(0, len(macs), 2)
+        O.find_route_pair(db, macs[a], macs[b])
+        k += 1
+    dt = time.perf_counter() - t0
+    ref = {"value": k / dt, "unit": "routes/s", "cores": 1, "kind": "port",
+           "sample": "oracle.find_route_pair (per-pair Python LIFO search, the "
+                     "reference's algorithm shape) on %d random host pairs, %.2f s" % (k, dt)}
+    return out, ref
+
+
+class _DictDB(object):
+    def __init__(self):
+        self.switches, self.links, self.hosts = {}, {}, {}
+
+    def add_switch(self, s):
+        self.switches[s.dp.id] = s
+
+    def add_link(self, lk):
+        self.links.setdefault(lk.src.dpid, {})[lk.dst.dpid] = lk
+
+    def add_host(self, h):
+        self.hosts[h.mac] = h
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    fabric = T.by_name(args.fabric)
+    csr = fabric.csr()
+    V, E = csr.V, csr.E
+    hv, _ = fabric.host_table()
+    srcs, counts = np.unique(hv, return_counts=True)
+    srcs = srcs.astype(np.int32)
+    H = fabric.n_hosts
+    S = len(srcs)
+    per = (S + world - 1) // world
+    lo, hi = min(S, rank * per), min(S, (rank + 1) * per)
+    my = np.full(per, -1, np.int32)          # pad: out-of-range id -> empty row
+    my[: hi - lo] = srcs[lo:hi]
+
+    ctx = _native.Context(local)
+    ctx.upload(csr)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+    t_src = torch.from_numpy(my).to(dev)
+    if args.mode == "dfs":
+        a = torch.empty((per, V), dtype=torch.int32, device=dev)     # parent
+        b = torch.empty((per, V), dtype=torch.int32, device=dev)     # port
+        c = None
+    else:
+        a = torch.empty((per, V), dtype=torch.int16, device=dev)     # dist (u16)
+        b = torch.empty((per, V), dtype=torch.int32, device=dev)     # nh
+        c = torch.empty((per, V), dtype=torch.int32, device=dev)     # nh_port
+    if world > 1:
+        ga = torch.empty((world * per, V), dtype=a.dtype, device=dev)
+        gb = torch.empty((world * per, V), dtype=b.dtype, device=dev)
+        gc = torch.empty((world * per, V), dtype=c.dtype, device=dev) if c is not None else None
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        if args.mode == "dfs":
+            ctx.dfs_tables_device(t_src.data_ptr(), per, a.data_ptr(), b.data_ptr())
+        else:
+            ctx.shortest_tables_device(t_src.data_ptr(), per, a.data_ptr(), b.data_ptr(),
+                                       c.data_ptr())
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(ga, a)
+            dist.all_gather_into_tensor(gb, b)
+            if c is not None:
+                dist.all_gather_into_tensor(gc, c)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+
+    ms_per_step = elapsed / args.steps * 1e3
+    routes = float(H) * float(H)                 # every host pair, every step
+    value = routes / (ms_per_step / 1e3)
+    bytes_launch = algorithmic_bytes_per_source(V, E, args.mode) * (hi - lo)
+    achieved = bytes_launch / (kern_ms / 1e3) / 1e9
+    traffic = None
+    if os.path.exists(TRAFFIC_FILE):
+        try:
+            tf = json.load(open(TRAFFIC_FILE))
+            traffic = tf.get("%s/%s/N%d" % (args.fabric, args.mode, world))
+        except Exception:   # noqa: BLE001
+            traffic = None
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "routes/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (canonical fat-tree, SURVEY.md 8(d))",
+        "config": {
+            "workload": "%s all-pairs %s route tables (find_route%s)" % (
+                args.fabric, args.mode,
+                "" if args.mode == "dfs" else "(multiple=True)[0] + dist"),
+            "fabric": args.fabric, "V": V, "E": E, "hosts": H, "sources": S,
+            "host_pairs_per_step": int(routes),
+            "parallelism": "sources sharded over %d GPU(s)%s" % (
+                world, " + RCCL all-gather" if world > 1 else ""),
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "kernel": "dfs_lds_kernel" if args.mode == "dfs" else "msbfs+nexthop",
+            "kernel_ms": kern_ms, "bytes_per_launch": bytes_launch,
+        },
+        "switch_pair_routes_per_s": float(S) * V / (ms_per_step / 1e3),
+        "teps": float(hi - lo) * E / (kern_ms / 1e3),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "dfs":
+        base, ref = cpu_baseline(fabric, csr, srcs, counts, H, args.cpu_budget_s)
+        out["cpu_baseline"] = base
+        out["cpu_reference_path"] = ref
+        out["gpu_over_cpu"] = value / base["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

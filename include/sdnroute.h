@@ -1,0 +1,127 @@
+/*
+ * sdnroute.h -- C ABI of the MI355X route engine (libsdnroute.so).
+ *
+ * Drop-in boundary for the route hot path of keichi/sdn-mpi-router:
+ * the Python TopologyDB (reference sdnmpi/util/topology_db.py:8) keeps its
+ * API and dict state; its route computation is replaced by per-source /
+ * per-destination tables computed by the HIP kernels behind these entry
+ * points.  The reference has no FFI of its own (it is pure Python); these
+ * are the entry points a ctypes binding of that class binds (INTEGRATION.md
+ * shows the binding, sdn-mpi-router_amd/sdnmpi_amd/_native.py is ours).
+ *
+ * Conventions
+ *  - Every call returns SDNR_OK (0) or a negative errno-style code; the
+ *    message of the last failure on the calling thread is sdnr_last_error().
+ *  - Graph = dense CSR, vertex i = i-th smallest dpid, each row sorted
+ *    strictly ascending (== sorted(self.links[dpid].keys()),
+ *    topology_db.py:76), port[e] = links[u][v].src.port_no (:130).
+ *  - Tables are row-major [n_rows][V] int32 (dist: uint16); the caller owns
+ *    every buffer.  Without SDNR_DEVICE_PTRS they are host buffers and the
+ *    call is synchronous; with it they are device buffers on the context's
+ *    device and the call is asynchronous on the context's stream.
+ *  - Unreachable entries are SDNR_UNREACHED (-1) / SDNR_DIST_INF (0xFFFF).
+ *  - A context is not re-entrant (the reference calls TopologyDB from
+ *    Ryu's single OS thread); distinct contexts are independent.
+ */
+#ifndef SDNROUTE_H
+#define SDNROUTE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDNR_ABI_VERSION 1
+
+#define SDNR_OK          0
+#define SDNR_ERR_INVAL (-22)  /* EINVAL: bad argument / malformed CSR      */
+#define SDNR_ERR_NOMEM (-12)  /* ENOMEM: device or host allocation failed  */
+#define SDNR_ERR_NODEV (-19)  /* ENODEV: no such HIP device                */
+#define SDNR_ERR_STATE (-77)  /* EBADFD: no graph uploaded to the context  */
+#define SDNR_ERR_HIP   (-5)   /* EIO:    HIP runtime error                 */
+
+#define SDNR_DEVICE_PTRS 0x1u /* table/source pointers are device pointers */
+#define SDNR_TIMING      0x2u /* time the main kernel (sdnr_last_kernel_ms) */
+
+#define SDNR_UNREACHED (-1)
+#define SDNR_DIST_INF  0xFFFFu
+
+typedef struct sdnr_ctx sdnr_ctx;
+
+/* ABI version of the loaded library (== SDNR_ABI_VERSION it was built with) */
+int sdnr_abi_version(void);
+
+/* Message of the last failing call on this thread ("" if none). */
+const char *sdnr_last_error(void);
+
+/* Number of visible HIP devices. */
+int sdnr_device_count(int *count);
+
+/* Create / destroy a context bound to HIP device `device`.  The context owns
+ * the uploaded graph, scratch memory and a HIP stream.
+ * Replaces the state of TopologyDB.__init__ (topology_db.py:9-18). */
+int sdnr_create(int device, sdnr_ctx **out);
+int sdnr_destroy(sdnr_ctx *ctx);
+
+/* Run subsequent asynchronous work on `hip_stream` (a hipStream_t of the
+ * context's device, e.g. torch.cuda.current_stream().cuda_stream); NULL
+ * restores the context's own stream. */
+int sdnr_set_stream(sdnr_ctx *ctx, void *hip_stream);
+
+/* Wait for all work queued on the context's stream. */
+int sdnr_synchronize(sdnr_ctx *ctx);
+
+/* Upload the switch graph (host buffers).  Replaces the graph state that
+ * add_switch/add_link/delete_* maintain (topology_db.py:14-42); the Python
+ * side re-exports and re-uploads whenever that state changes.  Validates
+ * the CSR (monotone row_ptr, rows strictly ascending, 0 <= col < V). */
+int sdnr_graph_upload(sdnr_ctx *ctx, int32_t V, int32_t E,
+                      const int32_t *row_ptr, const int32_t *col,
+                      const int32_t *port);
+
+/* V, E and maximum out-degree of the uploaded graph (NULL fields skipped). */
+int sdnr_graph_info(const sdnr_ctx *ctx, int32_t *V, int32_t *E,
+                    int32_t *max_degree);
+
+/* Default route, find_route(src, dst) (multiple=False) -> _find_route_dfs
+ * (topology_db.py:59-84, called from :181-188), batched over all
+ * destinations: for every source src[i] the tree of first pushes of one full
+ * LIFO traversal.  Row i of each table (V entries):
+ *   parent[i*V+v]  vertex whose pop first pushed v (src[i] for v == src[i]),
+ *   port[i*V+v]    links[parent][v].src.port_no (-1 for the root),
+ *   hops[i*V+v]    tree depth (0 for the root); hops may be NULL.
+ * The route src -> d is the tree path; it equals the reference's route for
+ * every d, bit for bit (ports included). */
+int sdnr_dfs_tables(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc,
+                    int32_t *parent, int32_t *port, int32_t *hops,
+                    uint32_t flags);
+
+/* Shortest routes, find_route(src, dst, multiple=True) -> _find_routes_bfs
+ * (topology_db.py:86-122, called from :168-180), as per-destination tables:
+ * for every destination dst[i] and every vertex x
+ *   dist[i*V+x]     hop distance x -> dst[i] (SDNR_DIST_INF if none),
+ *   nh[i*V+x]       smallest out-neighbour n with dist(n) == dist(x) - 1
+ *                   (-1 for x == dst[i] or unreachable),
+ *   nh_port[i*V+x]  links[x][nh].src.port_no.
+ * Following nh from x gives routes[0] (the lexicographically smallest
+ * shortest path); the shortest-path DAG in dist gives the whole ECMP set in
+ * the reference's order.  nh / nh_port may be NULL (distances only). */
+int sdnr_shortest_tables(sdnr_ctx *ctx, const int32_t *dst, int32_t ndst,
+                         uint16_t *dist, int32_t *nh, int32_t *nh_port,
+                         uint32_t flags);
+
+/* All-pairs hop distances by blocked min-plus (Floyd-Warshall) closure for
+ * small dense graphs: dist[i*V+j] = hops i -> j (SDNR_DIST_INF if none).
+ * V <= 16384. */
+int sdnr_apsp(sdnr_ctx *ctx, uint16_t *dist, uint32_t flags);
+
+/* Device time in milliseconds of the main kernel(s) of the last table call
+ * made with SDNR_TIMING (waits for that call to finish). */
+int sdnr_last_kernel_ms(sdnr_ctx *ctx, float *ms);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SDNROUTE_H */

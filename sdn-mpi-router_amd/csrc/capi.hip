@@ -1,0 +1,338 @@
+// capi.hip -- extern "C" boundary of libsdnroute.so (include/sdnroute.h).
+//
+// Host side of the drop-in: validates and uploads the CSR the Python
+// TopologyDB exports from its dicts (reference sdnmpi/util/topology_db.py:
+// 14-18 state, :20-42 mutators), derives the ELL layout the DFS kernel reads,
+// stages host buffers when the caller passes host pointers, and forwards to
+// the kernel launchers (dfs.hip, shortest.hip, apsp.hip).
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "common.h"
+
+static thread_local char g_err[512] = "";
+
+int sdnr_fail(int code, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int sdnr_hip_fail(hipError_t e, const char *what)
+{
+    const int code = (e == hipErrorOutOfMemory) ? SDNR_ERR_NOMEM
+                     : (e == hipErrorInvalidDevice || e == hipErrorNoDevice) ? SDNR_ERR_NODEV
+                                                                             : SDNR_ERR_HIP;
+    return sdnr_fail(code, "%s: %s", what, hipGetErrorString(e));
+}
+
+int sdnr_reserve(void **buf, size_t *cur, size_t need)
+{
+    if (need <= *cur && *buf) return SDNR_OK;
+    if (*buf) {
+        (void)hipFree(*buf);
+        *buf = nullptr;
+        *cur = 0;
+    }
+    size_t n = need < 4096 ? 4096 : need;
+    hipError_t e = hipMalloc(buf, n);
+    if (e != hipSuccess) {
+        *buf = nullptr;
+        return sdnr_hip_fail(e, "hipMalloc(scratch)");
+    }
+    *cur = n;
+    return SDNR_OK;
+}
+
+static void free_graph(sdnr_ctx *c)
+{
+    int32_t **bufs[] = {&c->row_ptr, &c->col, &c->port, &c->ell_col, &c->ell_port};
+    for (int32_t **b : bufs) {
+        if (*b) (void)hipFree(*b);
+        *b = nullptr;
+    }
+    c->V = -1;
+    c->E = 0;
+    c->W = 0;
+    c->max_deg = 0;
+}
+
+static int upload(int32_t **dst, const void *src, size_t bytes, hipStream_t s)
+{
+    SDNR_HIP(hipMalloc(reinterpret_cast<void **>(dst), bytes < 4 ? 4 : bytes));
+    if (bytes) SDNR_HIP(hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, s));
+    return SDNR_OK;
+}
+
+#define CHECK_CTX(c) \
+    if (!(c)) return sdnr_fail(SDNR_ERR_INVAL, "%s: null context", __func__)
+
+extern "C" {
+
+int sdnr_abi_version(void) { return SDNR_ABI_VERSION; }
+
+const char *sdnr_last_error(void) { return g_err; }
+
+int sdnr_device_count(int *count)
+{
+    if (!count) return sdnr_fail(SDNR_ERR_INVAL, "sdnr_device_count: null count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e == hipErrorNoDevice) n = 0;
+    else if (e != hipSuccess) return sdnr_hip_fail(e, "hipGetDeviceCount");
+    *count = n;
+    return SDNR_OK;
+}
+
+int sdnr_create(int device, sdnr_ctx **out)
+{
+    if (!out) return sdnr_fail(SDNR_ERR_INVAL, "sdnr_create: null out");
+    *out = nullptr;
+    int n = 0;
+    int rc = sdnr_device_count(&n);
+    if (rc) return rc;
+    if (device < 0 || device >= n)
+        return sdnr_fail(SDNR_ERR_NODEV, "sdnr_create: device %d of %d", device, n);
+    SDNR_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    SDNR_HIP(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return sdnr_fail(SDNR_ERR_NODEV, "sdnr_create: device %d is %s, built for gfx950",
+                         device, prop.gcnArchName);
+    sdnr_ctx *c = new sdnr_ctx();
+    c->device = device;
+    c->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    if (e != hipSuccess) {
+        delete c;
+        return sdnr_hip_fail(e, "sdnr_create");
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return SDNR_OK;
+}
+
+int sdnr_destroy(sdnr_ctx *ctx)
+{
+    if (!ctx) return SDNR_OK;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    free_graph(ctx);
+    if (ctx->scratch) (void)hipFree(ctx->scratch);
+    if (ctx->stage) (void)hipFree(ctx->stage);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+    return SDNR_OK;
+}
+
+int sdnr_set_stream(sdnr_ctx *ctx, void *hip_stream)
+{
+    CHECK_CTX(ctx);
+    ctx->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+    return SDNR_OK;
+}
+
+int sdnr_synchronize(sdnr_ctx *ctx)
+{
+    CHECK_CTX(ctx);
+    SDNR_HIP(hipSetDevice(ctx->device));
+    SDNR_HIP(hipStreamSynchronize(ctx->stream));
+    return SDNR_OK;
+}
+
+int sdnr_graph_upload(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_ptr,
+                      const int32_t *col, const int32_t *port)
+{
+    CHECK_CTX(ctx);
+    if (V < 0 || E < 0) return sdnr_fail(SDNR_ERR_INVAL, "graph_upload: V=%d E=%d", V, E);
+    if (!row_ptr || (E > 0 && (!col || !port)))
+        return sdnr_fail(SDNR_ERR_INVAL, "graph_upload: null array");
+    if (row_ptr[0] != 0 || row_ptr[V] != E)
+        return sdnr_fail(SDNR_ERR_INVAL, "graph_upload: row_ptr[0]=%d row_ptr[V]=%d, E=%d",
+                         row_ptr[0], row_ptr[V], E);
+    int32_t maxdeg = 0;
+    for (int32_t u = 0; u < V; ++u) {
+        const int32_t a = row_ptr[u], b = row_ptr[u + 1];
+        if (b < a) return sdnr_fail(SDNR_ERR_INVAL, "graph_upload: row_ptr decreases at %d", u);
+        if (b - a > maxdeg) maxdeg = b - a;
+        for (int32_t e = a; e < b; ++e) {
+            if (col[e] < 0 || col[e] >= V)
+                return sdnr_fail(SDNR_ERR_INVAL, "graph_upload: col[%d]=%d out of range", e,
+                                 col[e]);
+            if (e > a && col[e] <= col[e - 1])
+                return sdnr_fail(SDNR_ERR_INVAL,
+                                 "graph_upload: row %d not strictly ascending at %d", u, e);
+        }
+    }
+    SDNR_HIP(hipSetDevice(ctx->device));
+    SDNR_HIP(hipStreamSynchronize(ctx->stream));
+    free_graph(ctx);
+    int rc;
+    if ((rc = upload(&ctx->row_ptr, row_ptr, sizeof(int32_t) * ((size_t)V + 1), ctx->stream)) ||
+        (rc = upload(&ctx->col, col, sizeof(int32_t) * (size_t)E, ctx->stream)) ||
+        (rc = upload(&ctx->port, port, sizeof(int32_t) * (size_t)E, ctx->stream))) {
+        free_graph(ctx);
+        return rc;
+    }
+    // ELL copy for the DFS chain: row u at u*W, -1 padded, when every row
+    // fits one wavefront and padding at most doubles the adjacency
+    int32_t W = 0;
+    if (maxdeg > 0 && maxdeg <= SDNR_WAVE && (size_t)V * maxdeg <= 2 * (size_t)E + 64)
+        W = maxdeg;
+    if (const char *f = getenv("SDNROUTE_ELL"))   // debug/test knob: 0 = CSR only
+        if (!strcmp(f, "0")) W = 0;
+    if (W > 0) {
+        std::vector<int32_t> ec((size_t)V * W, -1), ep((size_t)V * W, -1);
+        for (int32_t u = 0; u < V; ++u)
+            for (int32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) {
+                ec[(size_t)u * W + (e - row_ptr[u])] = col[e];
+                ep[(size_t)u * W + (e - row_ptr[u])] = port[e];
+            }
+        if ((rc = upload(&ctx->ell_col, ec.data(), ec.size() * 4, ctx->stream)) ||
+            (rc = upload(&ctx->ell_port, ep.data(), ep.size() * 4, ctx->stream))) {
+            free_graph(ctx);
+            return rc;
+        }
+        SDNR_HIP(hipStreamSynchronize(ctx->stream));   // before ec/ep go away
+    } else {
+        SDNR_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    ctx->V = V;
+    ctx->E = E;
+    ctx->W = W;
+    ctx->max_deg = maxdeg;
+    return SDNR_OK;
+}
+
+int sdnr_graph_info(const sdnr_ctx *ctx, int32_t *V, int32_t *E, int32_t *max_degree)
+{
+    CHECK_CTX(ctx);
+    if (ctx->V < 0) return sdnr_fail(SDNR_ERR_STATE, "graph_info: no graph uploaded");
+    if (V) *V = ctx->V;
+    if (E) *E = ctx->E;
+    if (max_degree) *max_degree = ctx->max_deg;
+    return SDNR_OK;
+}
+
+// host <-> device staging for host-pointer calls
+struct Stage {
+    char *base = nullptr;
+    size_t off = 0;
+    void *take(size_t bytes)
+    {
+        void *p = base + off;
+        off += (bytes + 255) & ~(size_t)255;
+        return p;
+    }
+};
+
+static int begin_call(sdnr_ctx *ctx, int32_t n, const void *ids, uint32_t flags,
+                      const char *fn)
+{
+    if (!ctx) return sdnr_fail(SDNR_ERR_INVAL, "%s: null context", fn);
+    if (ctx->V < 0) return sdnr_fail(SDNR_ERR_STATE, "%s: no graph uploaded", fn);
+    if (n < 0) return sdnr_fail(SDNR_ERR_INVAL, "%s: negative count", fn);
+    if (n > 0 && !ids) return sdnr_fail(SDNR_ERR_INVAL, "%s: null id array", fn);
+    if (!(flags & SDNR_DEVICE_PTRS) && ids) {
+        const int32_t *h = static_cast<const int32_t *>(ids);
+        for (int32_t i = 0; i < n; ++i)
+            if (h[i] < 0 || h[i] >= ctx->V)
+                return sdnr_fail(SDNR_ERR_INVAL, "%s: id[%d]=%d outside [0,%d)", fn, i, h[i],
+                                 ctx->V);
+    }
+    SDNR_HIP(hipSetDevice(ctx->device));
+    ctx->timed = (flags & SDNR_TIMING) != 0;
+    return SDNR_OK;
+}
+
+int sdnr_dfs_tables(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc, int32_t *parent,
+                    int32_t *port, int32_t *hops, uint32_t flags)
+{
+    int rc = begin_call(ctx, nsrc, src, flags, "sdnr_dfs_tables");
+    if (rc) return rc;
+    if (nsrc > 0 && (!parent || !port))
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_tables: null table");
+    if (flags & SDNR_DEVICE_PTRS) return sdnr_launch_dfs(ctx, src, nsrc, parent, port, hops);
+    const size_t V = (size_t)ctx->V, rows = (size_t)nsrc * V;
+    const size_t need = 4 * (size_t)nsrc + 256 + (rows * 4 + 256) * (hops ? 3 : 2);
+    if ((rc = sdnr_reserve(&ctx->stage, &ctx->stage_bytes, need))) return rc;
+    Stage st{static_cast<char *>(ctx->stage)};
+    int32_t *d_src = static_cast<int32_t *>(st.take(4 * (size_t)nsrc));
+    int32_t *d_par = static_cast<int32_t *>(st.take(rows * 4));
+    int32_t *d_prt = static_cast<int32_t *>(st.take(rows * 4));
+    int32_t *d_hop = hops ? static_cast<int32_t *>(st.take(rows * 4)) : nullptr;
+    SDNR_HIP(hipMemcpyAsync(d_src, src, 4 * (size_t)nsrc, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = sdnr_launch_dfs(ctx, d_src, nsrc, d_par, d_prt, d_hop))) return rc;
+    SDNR_HIP(hipMemcpyAsync(parent, d_par, rows * 4, hipMemcpyDeviceToHost, ctx->stream));
+    SDNR_HIP(hipMemcpyAsync(port, d_prt, rows * 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (hops) SDNR_HIP(hipMemcpyAsync(hops, d_hop, rows * 4, hipMemcpyDeviceToHost, ctx->stream));
+    SDNR_HIP(hipStreamSynchronize(ctx->stream));
+    return SDNR_OK;
+}
+
+int sdnr_shortest_tables(sdnr_ctx *ctx, const int32_t *dst, int32_t ndst, uint16_t *dist,
+                         int32_t *nh, int32_t *nh_port, uint32_t flags)
+{
+    int rc = begin_call(ctx, ndst, dst, flags, "sdnr_shortest_tables");
+    if (rc) return rc;
+    if (ndst > 0 && !dist) return sdnr_fail(SDNR_ERR_INVAL, "sdnr_shortest_tables: null dist");
+    if ((nh == nullptr) != (nh_port == nullptr))
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_shortest_tables: nh and nh_port go together");
+    if (flags & SDNR_DEVICE_PTRS) return sdnr_launch_shortest(ctx, dst, ndst, dist, nh, nh_port);
+    const size_t V = (size_t)ctx->V, rows = (size_t)ndst * V;
+    const size_t need = 4 * (size_t)ndst + 256 + rows * 2 + 256 + (nh ? 2 * (rows * 4 + 256) : 0);
+    if ((rc = sdnr_reserve(&ctx->stage, &ctx->stage_bytes, need))) return rc;
+    Stage st{static_cast<char *>(ctx->stage)};
+    int32_t *d_dst = static_cast<int32_t *>(st.take(4 * (size_t)ndst));
+    uint16_t *d_dist = static_cast<uint16_t *>(st.take(rows * 2));
+    int32_t *d_nh = nh ? static_cast<int32_t *>(st.take(rows * 4)) : nullptr;
+    int32_t *d_np = nh ? static_cast<int32_t *>(st.take(rows * 4)) : nullptr;
+    SDNR_HIP(hipMemcpyAsync(d_dst, dst, 4 * (size_t)ndst, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = sdnr_launch_shortest(ctx, d_dst, ndst, d_dist, d_nh, d_np))) return rc;
+    SDNR_HIP(hipMemcpyAsync(dist, d_dist, rows * 2, hipMemcpyDeviceToHost, ctx->stream));
+    if (nh) {
+        SDNR_HIP(hipMemcpyAsync(nh, d_nh, rows * 4, hipMemcpyDeviceToHost, ctx->stream));
+        SDNR_HIP(hipMemcpyAsync(nh_port, d_np, rows * 4, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    SDNR_HIP(hipStreamSynchronize(ctx->stream));
+    return SDNR_OK;
+}
+
+int sdnr_apsp(sdnr_ctx *ctx, uint16_t *dist, uint32_t flags)
+{
+    int rc = begin_call(ctx, 0, nullptr, flags, "sdnr_apsp");
+    if (rc) return rc;
+    if (!dist) return sdnr_fail(SDNR_ERR_INVAL, "sdnr_apsp: null dist");
+    if (flags & SDNR_DEVICE_PTRS) return sdnr_launch_apsp(ctx, dist);
+    const size_t bytes = (size_t)ctx->V * ctx->V * 2;
+    if ((rc = sdnr_reserve(&ctx->stage, &ctx->stage_bytes, bytes))) return rc;
+    uint16_t *d = static_cast<uint16_t *>(ctx->stage);
+    if ((rc = sdnr_launch_apsp(ctx, d))) return rc;
+    SDNR_HIP(hipMemcpyAsync(dist, d, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    SDNR_HIP(hipStreamSynchronize(ctx->stream));
+    return SDNR_OK;
+}
+
+int sdnr_last_kernel_ms(sdnr_ctx *ctx, float *ms)
+{
+    CHECK_CTX(ctx);
+    if (!ms) return sdnr_fail(SDNR_ERR_INVAL, "sdnr_last_kernel_ms: null ms");
+    if (!ctx->timed) return sdnr_fail(SDNR_ERR_STATE, "sdnr_last_kernel_ms: last call untimed");
+    SDNR_HIP(hipSetDevice(ctx->device));
+    SDNR_HIP(hipEventSynchronize(ctx->ev1));
+    SDNR_HIP(hipEventElapsedTime(ms, ctx->ev0, ctx->ev1));
+    return SDNR_OK;
+}
+
+}  // extern "C"

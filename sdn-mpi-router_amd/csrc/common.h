@@ -1,0 +1,77 @@
+// common.h -- shared device helpers and the context layout of libsdnroute.
+// gfx950 (CDNA4) only: 64-lane wavefronts, 160 KiB LDS per CU, 256 CUs.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/sdnroute.h"
+
+#define SDNR_WAVE 64
+#define SDNR_LDS_PER_CU (160 * 1024)
+#define SDNR_MAX_LDS_PER_BLOCK (160 * 1024)
+
+// ---------------------------------------------------------------- device --
+
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+// number of set bits of m strictly below this lane
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ int uniform(int x) {
+    return __builtin_amdgcn_readfirstlane(x);
+}
+
+__device__ __forceinline__ int read_lane(int x, int lane) {
+    return __builtin_amdgcn_readlane(x, lane);
+}
+
+__device__ __forceinline__ int highest_lane(uint64_t m) { return 63 - __clzll(m); }
+
+// ------------------------------------------------------------------ host --
+
+struct sdnr_ctx {
+    int device = 0;
+    int num_cus = 256;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+
+    // graph (device)
+    int32_t V = -1, E = 0, max_deg = 0;
+    int32_t W = 0;                      // ELL row width (0: CSR only)
+    int32_t *row_ptr = nullptr, *col = nullptr, *port = nullptr;
+    int32_t *ell_col = nullptr, *ell_port = nullptr;
+
+    // grow-only device scratch / staging
+    void *scratch = nullptr;
+    size_t scratch_bytes = 0;
+    void *stage = nullptr;
+    size_t stage_bytes = 0;
+
+    // timing of the main kernel(s) of the last SDNR_TIMING call
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+};
+
+// error plumbing (capi.hip)
+int sdnr_fail(int code, const char *fmt, ...);
+int sdnr_hip_fail(hipError_t e, const char *what);
+int sdnr_reserve(void **buf, size_t *cur, size_t need);
+
+#define SDNR_HIP(call)                                           \
+    do {                                                         \
+        hipError_t _e = (call);                                  \
+        if (_e != hipSuccess) return sdnr_hip_fail(_e, #call);   \
+    } while (0)
+
+// kernel launchers (dfs.hip, shortest.hip, apsp.hip); device pointers,
+// asynchronous on ctx->stream
+int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
+                    int32_t *d_parent, int32_t *d_port, int32_t *d_hops);
+int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
+                         uint16_t *d_dist, int32_t *d_nh, int32_t *d_nh_port);
+int sdnr_launch_apsp(sdnr_ctx *ctx, uint16_t *d_dist);

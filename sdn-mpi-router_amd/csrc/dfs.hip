@@ -1,0 +1,359 @@
+// dfs.hip -- reference-exact default-route tables on gfx950.
+//
+// Reference: TopologyDB._find_route_dfs (sdnmpi/util/topology_db.py:59-84):
+// a LIFO stack search where a switch is marked visited when it is PUSHED
+// (:78-82) and neighbours are pushed in ascending dpid order (:76).  The
+// parent of v is fixed by the pop that first pushes it, and stopping at the
+// destination (:70-71) happens after that push, so one full traversal from
+// s answers find_route(s, d) for EVERY d: the route is the path from s to d
+// in the tree of first pushes.  That traversal is serial pop after pop, so
+// the kernels run one source per wavefront and make the pop chain short:
+//
+//  * one pop = one coalesced load of u's adjacency row (ELL rows of width
+//    W <= 64 are addressed as u*W: no row_ptr load on the chain), a gather of
+//    the visited bits from LDS, __ballot over the row, mbcnt ranks for the
+//    ascending push order, and ds_or to mark;
+//  * the largest freshly pushed child is the next pop (LIFO), so it stays in
+//    an SGPR instead of going through the stack;
+//  * dfs_lds_kernel (V < 65536, small graphs): visited bits, stack, parent,
+//    slot and depth live in LDS (10 B per vertex) and the tables are written
+//    once, coalesced, after the traversal -- no global store on the chain;
+//  * dfs_global_kernel (large graphs): visited bits and a 1024-entry stack
+//    ring in LDS, spilled to / refilled from global scratch in halves;
+//    table entries are stored as vertices are pushed.
+//
+// Sources are independent: persistent grid, one 64-thread workgroup per
+// source, grid-stride over sources.
+#include <stdlib.h>
+#include <string.h>
+
+#include "common.h"
+
+namespace {
+
+constexpr int kRing = 1024;   // LDS stack ring entries (global mode)
+
+template <bool ELL, bool HOPS>
+__global__ __launch_bounds__(64) void dfs_lds_kernel(
+    int V, int W, const int32_t *__restrict__ row_ptr,
+    const int32_t *__restrict__ col, const int32_t *__restrict__ port,
+    const int32_t *__restrict__ src, int nsrc, int32_t *__restrict__ out_parent,
+    int32_t *__restrict__ out_port, int32_t *__restrict__ out_hops)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int VW = (V + 31) >> 5;
+    const int VWp = (VW + 3) & ~3;
+    uint32_t *vis = lds;                       // visited bits
+    uint32_t *stk = vis + VWp;                 // stack: v | depth << 16
+    uint32_t *ps = stk + V;                    // parent | row slot << 16
+    uint16_t *dep = reinterpret_cast<uint16_t *>(ps + V);
+    const int lane = lane_id();
+
+    for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
+        const int s = uniform(src[si]);
+        int32_t *prow = out_parent + (size_t)si * V;
+        int32_t *trow = out_port + (size_t)si * V;
+        int32_t *hrow = HOPS ? out_hops + (size_t)si * V : nullptr;
+        if (s < 0 || s >= V) {                 // unknown source: empty row
+            for (int v = lane; v < V; v += SDNR_WAVE) {
+                prow[v] = -1;
+                trow[v] = -1;
+                if (HOPS) hrow[v] = -1;
+            }
+            continue;
+        }
+        for (int w = lane; w < VW; w += SDNR_WAVE) vis[w] = 0u;
+        __syncthreads();
+        if (lane == 0) {
+            vis[s >> 5] = 1u << (s & 31);
+            ps[s] = (uint32_t)s;
+            dep[s] = 0;
+        }
+        __syncthreads();
+
+        int sp = 0, u = s, du = 0;
+        for (;;) {
+            int rs, re;
+            if (ELL) {
+                rs = u * W;
+                re = rs + W;
+            } else {
+                rs = row_ptr[u];
+                re = row_ptr[u + 1];
+            }
+            int nxt = -1;
+            for (int base = rs; base < re; base += SDNR_WAVE) {
+                const int e = base + lane;
+                int v = -1;
+                if (e < re) v = col[e];
+                bool unv = false;
+                if (v >= 0) unv = ((vis[v >> 5] >> (v & 31)) & 1u) == 0u;
+                const uint64_t m = __ballot(unv);
+                if (m == 0) continue;
+                const int cnt = __popcll(m);
+                const int rank = lanes_below(m);
+                const uint32_t dtag = (uint32_t)(du + 1) << 16;
+                if (nxt >= 0) {                // previous chunk's top goes below
+                    if (lane == 0) stk[sp] = (uint32_t)nxt | dtag;
+                    sp += 1;
+                }
+                if (unv) {
+                    atomicOr(&vis[v >> 5], 1u << (v & 31));
+                    ps[v] = (uint32_t)u | ((uint32_t)(e - rs) << 16);
+                    if (HOPS) dep[v] = (uint16_t)(du + 1);
+                    if (rank < cnt - 1) stk[sp + rank] = (uint32_t)v | dtag;
+                }
+                sp += cnt - 1;
+                nxt = read_lane(v, highest_lane(m));
+            }
+            if (nxt >= 0) {
+                u = nxt;
+                du += 1;
+            } else {
+                if (sp == 0) break;
+                sp -= 1;
+                const uint32_t ent = (uint32_t)uniform((int)stk[sp]);
+                u = (int)(ent & 0xFFFFu);
+                du = (int)(ent >> 16);
+            }
+        }
+        __syncthreads();
+
+        for (int v = lane; v < V; v += SDNR_WAVE) {
+            int p = -1, pt = -1, h = -1;
+            if ((vis[v >> 5] >> (v & 31)) & 1u) {
+                const uint32_t x = ps[v];
+                p = (int)(x & 0xFFFFu);
+                if (v == s) {
+                    h = 0;
+                } else {
+                    const int slot = (int)(x >> 16);
+                    pt = ELL ? port[(size_t)p * W + slot] : port[row_ptr[p] + slot];
+                    h = HOPS ? (int)dep[v] : 0;
+                }
+            }
+            prow[v] = p;
+            trow[v] = pt;
+            if (HOPS) hrow[v] = h;
+        }
+        __syncthreads();
+    }
+}
+
+template <bool ELL, bool HOPS>
+__global__ __launch_bounds__(64) void dfs_global_kernel(
+    int V, int W, const int32_t *__restrict__ row_ptr,
+    const int32_t *__restrict__ col, const int32_t *__restrict__ port,
+    const int32_t *__restrict__ src, int nsrc, int32_t *__restrict__ out_parent,
+    int32_t *__restrict__ out_port, int32_t *__restrict__ out_hops,
+    uint2 *__restrict__ spill_all)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int VW = (V + 31) >> 5;
+    const int VWp = (VW + 3) & ~3;
+    uint32_t *vis = lds;
+    uint2 *ring = reinterpret_cast<uint2 *>(vis + VWp);   // (v, depth)
+    uint2 *spill = spill_all + (size_t)blockIdx.x * (size_t)V;
+    const int lane = lane_id();
+
+    for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
+        const int s = uniform(src[si]);
+        int32_t *prow = out_parent + (size_t)si * V;
+        int32_t *trow = out_port + (size_t)si * V;
+        int32_t *hrow = HOPS ? out_hops + (size_t)si * V : nullptr;
+        if (s < 0 || s >= V) {
+            for (int v = lane; v < V; v += SDNR_WAVE) {
+                prow[v] = -1;
+                trow[v] = -1;
+                if (HOPS) hrow[v] = -1;
+            }
+            continue;
+        }
+        for (int w = lane; w < VW; w += SDNR_WAVE) vis[w] = 0u;
+        __syncthreads();
+        if (lane == 0) {
+            vis[s >> 5] = 1u << (s & 31);
+            prow[s] = s;
+            trow[s] = -1;
+            if (HOPS) hrow[s] = 0;
+        }
+        __syncthreads();
+
+        int lsp = 0, bot = 0, gsp = 0;        // ring depth, ring bottom, spilled
+        int u = s, du = 0;
+        for (;;) {
+            int rs, re;
+            if (ELL) {
+                rs = u * W;
+                re = rs + W;
+            } else {
+                rs = row_ptr[u];
+                re = row_ptr[u + 1];
+            }
+            int nxt = -1;
+            for (int base = rs; base < re; base += SDNR_WAVE) {
+                const int e = base + lane;
+                int v = -1, pt = -1;
+                if (e < re) {
+                    v = col[e];
+                    pt = port[e];
+                }
+                bool unv = false;
+                if (v >= 0) unv = ((vis[v >> 5] >> (v & 31)) & 1u) == 0u;
+                const uint64_t m = __ballot(unv);
+                if (m == 0) continue;
+                const int cnt = __popcll(m);
+                const int rank = lanes_below(m);
+                if (unv) {
+                    atomicOr(&vis[v >> 5], 1u << (v & 31));
+                    prow[v] = u;
+                    trow[v] = pt;
+                    if (HOPS) hrow[v] = du + 1;
+                }
+                if (lsp + cnt > kRing) {       // spill the oldest half
+                    for (int i = lane; i < kRing / 2; i += SDNR_WAVE)
+                        spill[gsp + i] = ring[(bot + i) & (kRing - 1)];
+                    gsp += kRing / 2;
+                    bot = (bot + kRing / 2) & (kRing - 1);
+                    lsp -= kRing / 2;
+                }
+                const uint32_t dn = (uint32_t)(du + 1);
+                if (nxt >= 0) {
+                    if (lane == 0) ring[(bot + lsp) & (kRing - 1)] = make_uint2((uint32_t)nxt, dn);
+                    lsp += 1;
+                }
+                if (unv && rank < cnt - 1)
+                    ring[(bot + lsp + rank) & (kRing - 1)] = make_uint2((uint32_t)v, dn);
+                lsp += cnt - 1;
+                nxt = read_lane(v, highest_lane(m));
+            }
+            if (nxt >= 0) {
+                u = nxt;
+                du += 1;
+                continue;
+            }
+            if (lsp == 0) {
+                if (gsp == 0) break;
+                const int n = gsp < kRing / 2 ? gsp : kRing / 2;
+                // the spill was written by this wave: wait for the stores and
+                // drop this CU's L1 copy before reading it back
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                bot = (bot - n) & (kRing - 1);
+                for (int i = lane; i < n; i += SDNR_WAVE)
+                    ring[(bot + i) & (kRing - 1)] = spill[gsp - n + i];
+                gsp -= n;
+                lsp = n;
+            }
+            lsp -= 1;
+            const uint2 ent = ring[(bot + lsp) & (kRing - 1)];
+            u = uniform((int)ent.x);
+            du = uniform((int)ent.y);
+        }
+        __syncthreads();
+        for (int v = lane; v < V; v += SDNR_WAVE) {
+            if (((vis[v >> 5] >> (v & 31)) & 1u) == 0u) {
+                prow[v] = -1;
+                trow[v] = -1;
+                if (HOPS) hrow[v] = -1;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <typename K>
+void allow_full_lds(K kernel)
+{
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              SDNR_MAX_LDS_PER_BLOCK);
+}
+
+size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+}  // namespace
+
+// LDS bytes per source of the two strategies (also used by the host-side
+// planner through sdnr_launch_dfs)
+static size_t dfs_lds_bytes_small(int V)
+{
+    const size_t VWp = (size_t)((((V + 31) >> 5) + 3) & ~3);
+    return align16(4 * VWp + 8 * (size_t)V + 2 * (size_t)V);
+}
+
+static size_t dfs_lds_bytes_global(int V)
+{
+    const size_t VWp = (size_t)((((V + 31) >> 5) + 3) & ~3);
+    return align16(4 * VWp + 8 * (size_t)kRing);
+}
+
+int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
+                    int32_t *d_parent, int32_t *d_port, int32_t *d_hops)
+{
+    const int V = ctx->V;
+    if (nsrc == 0 || V == 0) return SDNR_OK;
+    const bool ell = ctx->W > 0;
+    const bool hops = d_hops != nullptr;
+    const int W = ctx->W;
+    const size_t small_b = dfs_lds_bytes_small(V);
+    const size_t cu_blocks_small = SDNR_LDS_PER_CU / small_b;
+    bool small = V < 65536 && small_b <= 64 * 1024 &&
+                 (small_b <= 40 * 1024 ||
+                  (size_t)nsrc <= (size_t)ctx->num_cus * cu_blocks_small);
+    // debug/test knob: SDNROUTE_DFS_STRATEGY=lds|global forces a strategy
+    if (const char *f = getenv("SDNROUTE_DFS_STRATEGY")) {
+        if (!strcmp(f, "global")) small = false;
+        else if (!strcmp(f, "lds") && V < 65536 && small_b <= SDNR_MAX_LDS_PER_BLOCK) small = true;
+    }
+    if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
+    if (small) {
+        size_t bpc = cu_blocks_small < 16 ? cu_blocks_small : 16;
+        if (bpc < 1) bpc = 1;
+        int grid = (int)((size_t)ctx->num_cus * bpc);
+        if (grid > nsrc) grid = nsrc;
+#define SDNR_DFS_SMALL(E_, H_)                                                    \
+    do {                                                                          \
+        auto k = dfs_lds_kernel<E_, H_>;                                          \
+        allow_full_lds(k);                                                        \
+        hipLaunchKernelGGL(k, dim3(grid), dim3(64), small_b, ctx->stream, V, W,   \
+                           ctx->row_ptr, E_ ? ctx->ell_col : ctx->col,            \
+                           E_ ? ctx->ell_port : ctx->port, d_src, nsrc, d_parent, \
+                           d_port, d_hops);                                       \
+    } while (0)
+        if (ell && hops) SDNR_DFS_SMALL(true, true);
+        else if (ell) SDNR_DFS_SMALL(true, false);
+        else if (hops) SDNR_DFS_SMALL(false, true);
+        else SDNR_DFS_SMALL(false, false);
+#undef SDNR_DFS_SMALL
+    } else {
+        const size_t gb = dfs_lds_bytes_global(V);
+        if (gb > SDNR_MAX_LDS_PER_BLOCK)
+            return sdnr_fail(SDNR_ERR_INVAL, "graph too large for the LDS visited set (V=%d)", V);
+        size_t bpc = SDNR_LDS_PER_CU / gb;
+        if (bpc > 16) bpc = 16;
+        if (bpc < 1) bpc = 1;
+        int grid = (int)((size_t)ctx->num_cus * bpc);
+        if (grid > nsrc) grid = nsrc;
+        const size_t need = (size_t)grid * (size_t)V * sizeof(uint2);
+        int rc = sdnr_reserve(&ctx->scratch, &ctx->scratch_bytes, need);
+        if (rc) return rc;
+        uint2 *spill = static_cast<uint2 *>(ctx->scratch);
+#define SDNR_DFS_GLOBAL(E_, H_)                                                   \
+    do {                                                                          \
+        auto k = dfs_global_kernel<E_, H_>;                                       \
+        allow_full_lds(k);                                                        \
+        hipLaunchKernelGGL(k, dim3(grid), dim3(64), gb, ctx->stream, V, W,        \
+                           ctx->row_ptr, E_ ? ctx->ell_col : ctx->col,            \
+                           E_ ? ctx->ell_port : ctx->port, d_src, nsrc, d_parent, \
+                           d_port, d_hops, spill);                                \
+    } while (0)
+        if (ell && hops) SDNR_DFS_GLOBAL(true, true);
+        else if (ell) SDNR_DFS_GLOBAL(true, false);
+        else if (hops) SDNR_DFS_GLOBAL(false, true);
+        else SDNR_DFS_GLOBAL(false, false);
+#undef SDNR_DFS_GLOBAL
+    }
+    SDNR_HIP(hipGetLastError());
+    if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+    return SDNR_OK;
+}

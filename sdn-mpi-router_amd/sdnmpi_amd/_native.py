@@ -1,0 +1,229 @@
+"""ctypes binding of libsdnroute.so (C ABI: include/sdnroute.h).
+
+This is the only way the product reaches the route kernels; there is no CPU
+fallback.  If the library is missing or no gfx950 device is visible the
+calls fail loudly (:class:`NativeUnavailable` / :class:`SdnrError`).
+
+PyTorch ROCm bundles its own ``libamdhip64.so.7``; when torch is importable
+it is imported first so that this library binds to the same HIP runtime
+(shared soname) and device pointers / streams can be exchanged with torch.
+"""
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+__all__ = ["NativeUnavailable", "SdnrError", "library", "library_path",
+           "Context", "DEVICE_PTRS", "TIMING", "UNREACHED", "DIST_INF",
+           "EXPORTED_SYMBOLS"]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_NAME = "libsdnroute.so"
+
+DEVICE_PTRS = 0x1
+TIMING = 0x2
+UNREACHED = -1
+DIST_INF = 0xFFFF
+ABI_VERSION = 1
+
+# every entry point declared in include/sdnroute.h
+EXPORTED_SYMBOLS = (
+    "sdnr_abi_version", "sdnr_last_error", "sdnr_device_count", "sdnr_create",
+    "sdnr_destroy", "sdnr_set_stream", "sdnr_synchronize", "sdnr_graph_upload",
+    "sdnr_graph_info", "sdnr_dfs_tables", "sdnr_shortest_tables", "sdnr_apsp",
+    "sdnr_last_kernel_ms",
+)
+
+
+class NativeUnavailable(RuntimeError):
+    """libsdnroute.so could not be loaded (not built, or no HIP runtime)."""
+
+
+class SdnrError(RuntimeError):
+    def __init__(self, code, msg):
+        super(SdnrError, self).__init__("sdnroute error %d: %s" % (code, msg))
+        self.code = code
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def library_path():
+    return os.environ.get("SDNROUTE_LIB", os.path.join(_HERE, _LIB_NAME))
+
+
+def _bind(L):
+    c_int, i32, u32, vp = ctypes.c_int, ctypes.c_int32, ctypes.c_uint32, ctypes.c_void_p
+    sig = {
+        "sdnr_abi_version": ([], c_int),
+        "sdnr_last_error": ([], ctypes.c_char_p),
+        "sdnr_device_count": ([ctypes.POINTER(c_int)], c_int),
+        "sdnr_create": ([c_int, ctypes.POINTER(vp)], c_int),
+        "sdnr_destroy": ([vp], c_int),
+        "sdnr_set_stream": ([vp, vp], c_int),
+        "sdnr_synchronize": ([vp], c_int),
+        "sdnr_graph_upload": ([vp, i32, i32, vp, vp, vp], c_int),
+        "sdnr_graph_info": ([vp, ctypes.POINTER(i32), ctypes.POINTER(i32),
+                             ctypes.POINTER(i32)], c_int),
+        "sdnr_dfs_tables": ([vp, vp, i32, vp, vp, vp, u32], c_int),
+        "sdnr_shortest_tables": ([vp, vp, i32, vp, vp, vp, u32], c_int),
+        "sdnr_apsp": ([vp, vp, u32], c_int),
+        "sdnr_last_kernel_ms": ([vp, ctypes.POINTER(ctypes.c_float)], c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    return L
+
+
+def library():
+    """Load (once) and return the bound library."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = library_path()
+        if not os.path.exists(path):
+            raise NativeUnavailable(
+                "%s not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                "in the repository root" % path)
+        try:   # share torch's HIP runtime when torch is around
+            import torch  # noqa: F401
+        except Exception:   # noqa: BLE001 - torch is optional plumbing
+            pass
+        try:
+            L = ctypes.CDLL(path)
+        except OSError as e:
+            raise NativeUnavailable("cannot load %s: %s" % (path, e))
+        _bind(L)
+        if L.sdnr_abi_version() != ABI_VERSION:
+            raise NativeUnavailable("ABI mismatch: library %d, binding %d"
+                                    % (L.sdnr_abi_version(), ABI_VERSION))
+        _lib = L
+        return L
+
+
+def _check(rc):
+    if rc != 0:
+        msg = library().sdnr_last_error().decode("utf-8", "replace")
+        raise SdnrError(rc, msg)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    _check(library().sdnr_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class Context(object):
+    """One route-engine context on one HIP device (owns graph + scratch)."""
+
+    def __init__(self, device=0):
+        self._lib = library()
+        h = ctypes.c_void_p()
+        _check(self._lib.sdnr_create(int(device), ctypes.byref(h)))
+        self._h = h
+        self.device = int(device)
+        self.V = -1
+        self.E = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.sdnr_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:   # noqa: BLE001 - interpreter shutdown
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- setup --------------------------------------------------------
+    def set_stream(self, stream_handle):
+        _check(self._lib.sdnr_set_stream(self._h, ctypes.c_void_p(stream_handle or 0)
+                                         if stream_handle else None))
+
+    def synchronize(self):
+        _check(self._lib.sdnr_synchronize(self._h))
+
+    def upload(self, csr):
+        rp = np.ascontiguousarray(csr.row_ptr, np.int32)
+        col = np.ascontiguousarray(csr.col, np.int32)
+        port = np.ascontiguousarray(csr.port, np.int32)
+        V, E = int(rp.shape[0] - 1), int(col.shape[0])
+        _check(self._lib.sdnr_graph_upload(self._h, V, E, _ptr(rp),
+                                           _ptr(col) if E else None,
+                                           _ptr(port) if E else None))
+        self.V, self.E = V, E
+
+    def info(self):
+        V, E, D = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        _check(self._lib.sdnr_graph_info(self._h, ctypes.byref(V), ctypes.byref(E),
+                                         ctypes.byref(D)))
+        return V.value, E.value, D.value
+
+    # -- host-buffer (synchronous) calls ------------------------------
+    def dfs_tables(self, srcs, with_hops=True):
+        srcs = np.ascontiguousarray(srcs, np.int32)
+        S, V = int(srcs.shape[0]), self.V
+        parent = np.empty((S, V), np.int32)
+        port = np.empty((S, V), np.int32)
+        hops = np.empty((S, V), np.int32) if with_hops else None
+        _check(self._lib.sdnr_dfs_tables(self._h, _ptr(srcs), S, _ptr(parent),
+                                         _ptr(port), _ptr(hops), 0))
+        return parent, port, hops
+
+    def shortest_tables(self, dsts, with_nexthop=True):
+        dsts = np.ascontiguousarray(dsts, np.int32)
+        D, V = int(dsts.shape[0]), self.V
+        dist = np.empty((D, V), np.uint16)
+        nh = np.empty((D, V), np.int32) if with_nexthop else None
+        nhp = np.empty((D, V), np.int32) if with_nexthop else None
+        _check(self._lib.sdnr_shortest_tables(self._h, _ptr(dsts), D, _ptr(dist),
+                                              _ptr(nh), _ptr(nhp), 0))
+        return dist, nh, nhp
+
+    def apsp(self):
+        dist = np.empty((self.V, self.V), np.uint16)
+        _check(self._lib.sdnr_apsp(self._h, _ptr(dist), 0))
+        return dist
+
+    # -- device-pointer (asynchronous) calls --------------------------
+    def dfs_tables_device(self, src_ptr, nsrc, parent_ptr, port_ptr, hops_ptr=0,
+                          timing=False):
+        flags = DEVICE_PTRS | (TIMING if timing else 0)
+        _check(self._lib.sdnr_dfs_tables(
+            self._h, ctypes.c_void_p(src_ptr), int(nsrc), ctypes.c_void_p(parent_ptr),
+            ctypes.c_void_p(port_ptr), ctypes.c_void_p(hops_ptr) if hops_ptr else None,
+            flags))
+
+    def shortest_tables_device(self, dst_ptr, ndst, dist_ptr, nh_ptr=0, nh_port_ptr=0,
+                               timing=False):
+        flags = DEVICE_PTRS | (TIMING if timing else 0)
+        _check(self._lib.sdnr_shortest_tables(
+            self._h, ctypes.c_void_p(dst_ptr), int(ndst), ctypes.c_void_p(dist_ptr),
+            ctypes.c_void_p(nh_ptr) if nh_ptr else None,
+            ctypes.c_void_p(nh_port_ptr) if nh_port_ptr else None, flags))
+
+    def apsp_device(self, dist_ptr, timing=False):
+        flags = DEVICE_PTRS | (TIMING if timing else 0)
+        _check(self._lib.sdnr_apsp(self._h, ctypes.c_void_p(dist_ptr), flags))
+
+    def last_kernel_ms(self):
+        ms = ctypes.c_float()
+        _check(self._lib.sdnr_last_kernel_ms(self._h, ctypes.byref(ms)))
+        return ms.value

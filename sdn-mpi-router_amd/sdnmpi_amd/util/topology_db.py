@@ -1,0 +1,251 @@
+"""Drop-in ``TopologyDB`` whose routes come from the MI355X route engine.
+
+Mirrors ``sdnmpi/util/topology_db.py`` of keichi/sdn-mpi-router: the same
+attributes (``switches``, ``links``, ``hosts`` dicts), mutators
+(``add_host``/``add_switch``/``delete_switch``/``add_link``/``delete_link``,
+:20-42), ``to_dict`` (:44-57) and ``find_route(src_mac, dst_mac,
+multiple=False)`` (:140-188) with the same return values and error
+behaviour: a list of ``(dpid, out_port)`` tuples, ``[]`` for unknown hosts
+or unreachable destinations, ``ValueError`` for a MAC that is not hex.
+
+What changes is how a route is found.  Instead of one Python stack search
+per (src, dst) pair, the switch graph is exported as a CSR and the GPU
+computes whole tables -- per source the tree of the reference's LIFO
+traversal (every destination at once), per destination the hop distances
+of the shortest-route mode -- which are cached until the dicts change and
+walked per query.  ``route_tables()`` / ``find_routes()`` expose the batched
+all-pairs form the MPI router needs.
+
+There is no CPU fallback: without ``libsdnroute.so`` or a gfx950 device the
+first route query raises (``sdnmpi_amd._native.NativeUnavailable`` /
+``SdnrError``).
+"""
+
+import numpy as np
+
+from ..engine import RouteEngine, TableCache, shortest_paths_lex, tree_path
+from ..graph import TrackedDict, Versions, export_graph
+
+try:   # the reference takes OFPP_LOCAL from Ryu's OpenFlow 1.0 module (:5)
+    from ryu.ofproto.ofproto_v1_0 import OFPP_LOCAL
+except Exception:   # noqa: BLE001 - Ryu is not a dependency of the engine
+    OFPP_LOCAL = 0xfffe
+
+__all__ = ["TopologyDB", "OFPP_LOCAL"]
+
+_INF = 0xFFFF
+
+
+class TopologyDB(object):
+    """Reference-compatible topology store with GPU route tables.
+
+    ``engine``: a :class:`~sdnmpi_amd.engine.RouteEngine` to share between
+    databases (default: one on HIP device ``device``, created lazily).
+    ``batch_sources``: when a table must be computed, compute it for every
+    host-bearing switch at once (the all-pairs batch) instead of only the
+    switch asked about.
+    """
+
+    def __init__(self, engine=None, device=0, batch_sources=True):
+        super(TopologyDB, self).__init__()
+        self._versions = Versions()
+        self._engine = engine
+        self._device = device
+        self._batch = batch_sources
+        self._export = None
+        self._cache = None
+        # Switch DPID -> Switch; src DPID -> dst DPID -> Link; MAC -> Host
+        self.switches = {}
+        self.links = {}
+        self.hosts = {}
+
+    # -- dict state (assignable, as the reference tests do) -----------
+    @property
+    def switches(self):
+        return self._switches
+
+    @switches.setter
+    def switches(self, d):
+        self._switches = TrackedDict(self._versions, "switches", d)
+
+    @property
+    def links(self):
+        return self._links
+
+    @links.setter
+    def links(self, d):
+        self._links = TrackedDict(self._versions, "links", d, nested=True)
+
+    @property
+    def hosts(self):
+        return self._hosts
+
+    @hosts.setter
+    def hosts(self, d):
+        self._hosts = TrackedDict(self._versions, "hosts", d)
+
+    # -- mutators (topology_db.py:20-42) -------------------------------
+    def add_host(self, host):
+        self.hosts[host.mac] = host
+
+    def add_switch(self, switch):
+        self.switches[switch.dp.id] = switch
+
+    def delete_switch(self, switch):
+        if switch.dp.id in self.switches:
+            del self.switches[switch.dp.id]
+
+    def add_link(self, link):
+        src_dpid = link.src.dpid
+        dst_dpid = link.dst.dpid
+        if src_dpid not in self.links:
+            self.links[src_dpid] = {}
+        self.links[src_dpid][dst_dpid] = link
+
+    def delete_link(self, link):
+        src_dpid = link.src.dpid
+        dst_dpid = link.dst.dpid
+        if src_dpid in self.links and dst_dpid in self.links[src_dpid]:
+            del self.links[src_dpid][dst_dpid]
+
+    def to_dict(self):
+        """JSON-serialisable snapshot (topology_db.py:44-57)."""
+        return {
+            "switches": [s.to_dict() for s in self.switches.values()],
+            "links": [lk.to_dict() for nb in self.links.values() for lk in nb.values()],
+            "hosts": [h.to_dict() for h in self.hosts.values()],
+        }
+
+    # -- engine / cache ------------------------------------------------
+    @property
+    def engine(self):
+        if self._engine is None:
+            self._engine = RouteEngine(self._device)
+        return self._engine
+
+    def graph(self):
+        """Current CSR export (re-exported after any dict mutation)."""
+        key = self._versions.key()
+        ex = self._export
+        if ex is None or ex.key != key:
+            new = export_graph(self.links, self.switches, self.hosts, key)
+            if ex is not None and _same_graph(ex.csr, new.csr):
+                ex.key = key             # only host ports / MACs changed
+            else:
+                self._export = ex = new
+                self._cache = TableCache(new)
+        return ex
+
+    def _host_vertices(self, ex):
+        idx = ex.index
+        return sorted({idx[h.port.dpid] for h in self.hosts.values()})
+
+    def _dfs(self, ex, s):
+        batch = self._host_vertices(ex) if self._batch and self._cache.dfs is None else ()
+        tabs = self._cache.dfs_rows(self.engine, [s], batch)
+        r = self._cache.dfs_row[s]
+        return tabs[0][r], tabs[1][r]
+
+    def _dist(self, ex, d):
+        batch = self._host_vertices(ex) if self._batch and self._cache.sp is None else ()
+        tabs = self._cache.sp_rows(self.engine, [d], batch)
+        return tabs[0][self._cache.sp_row[d]]
+
+    # -- route lookup (topology_db.py:124-188) ---------------------------
+    def _mac_to_int(self, mac):
+        return int(mac.replace(":", ""), 16)
+
+    def _endpoint(self, mac):
+        """(dpid, is_local) for a MAC, or None when it is neither a switch
+        local port nor a known host (topology_db.py:143-166)."""
+        if self._mac_to_int(mac) in self.switches:
+            return self._mac_to_int(mac), True
+        if mac not in self.hosts:
+            return None
+        return self.hosts[mac].port.dpid, False
+
+    def _last_hop(self, dst_dpid, dst_local, dst_mac):
+        if dst_local:
+            return (dst_dpid, OFPP_LOCAL)
+        return (dst_dpid, self.hosts[dst_mac].port.port_no)
+
+    def find_route(self, src_mac, dst_mac, multiple=False):
+        """Route between two hosts (or switch-local ports) as a list of
+        (datapath id, output port); with ``multiple=True`` the list of every
+        shortest route in the reference's order."""
+        s_local = self._mac_to_int(src_mac) in self.switches
+        d_local = self._mac_to_int(dst_mac) in self.switches
+        if not s_local and src_mac not in self.hosts:
+            return []
+        elif not d_local and dst_mac not in self.hosts:
+            return []
+        src_dpid = self._mac_to_int(src_mac) if s_local else self.hosts[src_mac].port.dpid
+        dst_dpid = self._mac_to_int(dst_mac) if d_local else self.hosts[dst_mac].port.dpid
+
+        ex = self.graph()
+        s, d = ex.index[src_dpid], ex.index[dst_dpid]
+        dpids = ex.csr.dpids
+        last = self._last_hop(dst_dpid, d_local, dst_mac)
+        if multiple:
+            seqs = shortest_paths_lex(ex.csr.row_ptr, ex.csr.col, self._dist(ex, d), s, d)
+            return [self._seq_fdb(ex, q, last) for q in seqs]
+        parent_row, port_row = self._dfs(ex, s)
+        seq = tree_path(parent_row, s, d)
+        if not seq:
+            return []
+        fdb = [(int(dpids[a]), int(port_row[b])) for a, b in zip(seq, seq[1:])]
+        fdb.append(last)
+        return fdb
+
+    def _seq_fdb(self, ex, seq, last):
+        c, out = ex.csr, []
+        for a, b in zip(seq, seq[1:]):
+            lo, hi = int(c.row_ptr[a]), int(c.row_ptr[a + 1])
+            e = lo + int(np.searchsorted(c.col[lo:hi], b))
+            out.append((int(c.dpids[a]), int(c.port[e])))
+        out.append(last)
+        return out
+
+    # -- batched (all-pairs) interface ---------------------------------
+    def route_tables(self, mode="dfs"):
+        """Tables for every host-bearing switch.
+
+        ``mode="dfs"``: per-source trees of the default route,
+        dict(sources, parent, port, hops, dpids);  ``mode="shortest"``:
+        per-destination dict(destinations, dist, nh, nh_port, dpids).
+        """
+        ex = self.graph()
+        hv = self._host_vertices(ex)
+        if mode == "dfs":
+            tabs = self._cache.dfs_rows(self.engine, hv)
+            rows = [self._cache.dfs_row[v] for v in hv]
+            return {"sources": np.asarray(hv, np.int32), "parent": tabs[0][rows],
+                    "port": tabs[1][rows], "hops": tabs[2][rows],
+                    "dpids": ex.csr.dpids}
+        if mode == "shortest":
+            tabs = self._cache.sp_rows(self.engine, hv)
+            rows = [self._cache.sp_row[v] for v in hv]
+            return {"destinations": np.asarray(hv, np.int32), "dist": tabs[0][rows],
+                    "nh": tabs[1][rows], "nh_port": tabs[2][rows],
+                    "dpids": ex.csr.dpids}
+        raise ValueError("mode must be 'dfs' or 'shortest'")
+
+    def find_routes(self, pairs, multiple=False):
+        """find_route over many (src_mac, dst_mac) pairs; tables are computed
+        once for all of them."""
+        pairs = list(pairs)
+        if not multiple and self._batch:
+            ex = self.graph()
+            want = set()
+            for a, _ in pairs:
+                ep = self._endpoint(a)
+                if ep is not None:
+                    want.add(ex.index[ep[0]])
+            self._cache.dfs_rows(self.engine, sorted(want), self._host_vertices(ex))
+        return [self.find_route(a, b, multiple) for a, b in pairs]
+
+
+def _same_graph(a, b):
+    return (a.V == b.V and a.E == b.E and np.array_equal(a.dpids, b.dpids)
+            and np.array_equal(a.row_ptr, b.row_ptr) and np.array_equal(a.col, b.col)
+            and np.array_equal(a.port, b.port))

@@ -1,0 +1,275 @@
+"""HIP tables vs the oracle, through the C ABI, on a gfx950 device.
+
+Bit-exact for every table (integer work): parent/port/hops of the default
+route, dist/nh/nh_port of the shortest mode, the APSP matrix.  Small fabrics
+are checked over ALL vertices as sources/destinations, the full-size
+BASELINE fabrics over all host-bearing sources (k=48, dragonfly) or a spread
+sample (torus 32^3, Jellyfish 100k) plus the reference's own sampled pairs.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import golden_util as G
+from oracle import oracle as O
+from sdnmpi_amd import _native
+from sdnmpi_amd import topologies as T
+
+pytestmark = pytest.mark.gpu
+
+NTHREADS = min(16, os.cpu_count() or 1)
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = _native.Context(0)
+    yield c
+    c.close()
+
+
+def _strategy(monkeypatch, dfs=None, ell=None):
+    if dfs:
+        monkeypatch.setenv("SDNROUTE_DFS_STRATEGY", dfs)
+    if ell is not None:
+        monkeypatch.setenv("SDNROUTE_ELL", "1" if ell else "0")
+
+
+def _check_dfs(ctx, csr, srcs, hops=True):
+    ctx.upload(csr)
+    p, t, h = ctx.dfs_tables(srcs, with_hops=hops)
+    po, to, ho = O.dfs_tables(csr, srcs, with_hops=hops, nthreads=NTHREADS)
+    np.testing.assert_array_equal(p, po)
+    np.testing.assert_array_equal(t, to)
+    if hops:
+        np.testing.assert_array_equal(h, ho)
+    return p, t
+
+
+def _check_pairs(g, fabric, p, t, srcs):
+    csr = fabric.csr()
+    hv, hp = fabric.host_table()
+    row = {int(s): i for i, s in enumerate(srcs)}
+    for i in range(len(g)):
+        a, b = int(g.pair_src[i]), int(g.pair_dst[i])
+        r = row[int(hv[a])]
+        got = O.tree_fdb(csr, p[r], t[r], int(hv[a]), int(hv[b]), hp[b])
+        assert got == g.fdb(i), (g.name, i)
+
+
+@pytest.mark.parametrize("strategy", ["auto", "lds", "global"])
+@pytest.mark.parametrize("ell", [True, False])
+@pytest.mark.parametrize("name", G.SMALL)
+def test_dfs_small_all_sources(ctx, monkeypatch, name, strategy, ell):
+    _strategy(monkeypatch, None if strategy == "auto" else strategy, ell)
+    g = G.Golden(name)
+    fabric = g.fabric()
+    csr = fabric.csr()
+    srcs = np.arange(csr.V, dtype=np.int32)
+    p, t = _check_dfs(ctx, csr, srcs)
+    _check_pairs(g, fabric, p, t, srcs)
+
+
+def test_dfs_without_hops_and_repeated_sources(ctx):
+    csr = T.fat_tree(8).csr()
+    srcs = np.array([5, 5, 0, csr.V - 1, 17, 5], np.int32)
+    _check_dfs(ctx, csr, srcs, hops=False)
+
+
+@pytest.mark.parametrize("name", ["fat_tree_k48_sample", "dragonfly_a16_h8_p8_sample"])
+def test_dfs_fullsize_all_host_sources(ctx, name):
+    g = G.Golden(name)
+    fabric = g.fabric()
+    csr = fabric.csr()
+    srcs = np.unique(fabric.host_table()[0]).astype(np.int32)
+    p, t = _check_dfs(ctx, csr, srcs)
+    _check_pairs(g, fabric, p, t, srcs)
+
+
+@pytest.mark.parametrize("name,nsample", [("torus_32x32x32_sample", 384),
+                                          ("jellyfish_n100000_r16_sample", 48)])
+def test_dfs_fullsize_sampled_sources(ctx, name, nsample):
+    g = G.Golden(name)
+    fabric = g.fabric()
+    csr = fabric.csr()
+    hv, _ = fabric.host_table()
+    spread = np.linspace(0, csr.V - 1, nsample).astype(np.int32)
+    srcs = np.unique(np.concatenate([spread, hv[g.pair_src]])).astype(np.int32)
+    p, t = _check_dfs(ctx, csr, srcs, hops=False)
+    _check_pairs(g, fabric, p, t, srcs)
+
+
+def test_dfs_fullsize_tree_properties(ctx):
+    """Size-independent checks on the complete k=48 table: every reachable
+    vertex's parent chain ends at the source, hop counts are parent + 1,
+    ports are real ports of the parent's row."""
+    fabric = T.fat_tree(48)
+    csr = fabric.csr()
+    srcs = np.arange(csr.V, dtype=np.int32)
+    ctx.upload(csr)
+    p, t, h = ctx.dfs_tables(srcs)
+    V = csr.V
+    assert (p >= 0).all()                       # fat-tree is connected
+    r = np.arange(V)
+    assert (p[srcs, srcs] == srcs).all() and (h[srcs, srcs] == 0).all()
+    nonroot = p != r[None, :].repeat(len(srcs), 0)
+    nonroot[srcs, srcs] = False
+    hp = np.take_along_axis(h, p.astype(np.int64), 1)
+    assert (h[nonroot] == hp[nonroot] + 1).all()
+    # (parent, child) is a link and the port matches the CSR
+    rows = csr.row_ptr
+    for s in (0, 1, 777, V - 1):
+        for v in range(V):
+            if v == s:
+                continue
+            u = p[s, v]
+            lo, hi = rows[u], rows[u + 1]
+            k = lo + np.searchsorted(csr.col[lo:hi], v)
+            assert k < hi and csr.col[k] == v and csr.port[k] == t[s, v]
+
+
+@pytest.mark.parametrize("name", G.SMALL)
+def test_shortest_small_all_destinations(ctx, name):
+    fabric = G.Golden(name).fabric()
+    csr = fabric.csr()
+    dsts = np.arange(csr.V, dtype=np.int32)
+    ctx.upload(csr)
+    dist, nh, nhp = ctx.shortest_tables(dsts)
+    do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
+    np.testing.assert_array_equal(dist, do)
+    np.testing.assert_array_equal(nh, nho)
+    np.testing.assert_array_equal(nhp, nhpo)
+
+
+@pytest.mark.parametrize("name", G.MULTI)
+def test_shortest_matches_reference_multiple(ctx, name):
+    from sdnmpi_amd.engine import shortest_paths_lex
+    g = G.Golden(name)
+    fabric = g.fabric()
+    csr = fabric.csr()
+    hv, hp = fabric.host_table()
+    dsts = np.unique(hv).astype(np.int32)
+    ctx.upload(csr)
+    dist, nh, nhp = ctx.shortest_tables(dsts)
+    row = {int(d): i for i, d in enumerate(dsts)}
+    for i in range(len(g)):
+        a, b = int(g.pair_src[i]), int(g.pair_dst[i])
+        s, d = int(hv[a]), int(hv[b])
+        seqs = shortest_paths_lex(csr.row_ptr, csr.col, dist[row[d]], s, d)
+        want = g.multi(i)
+        assert len(seqs) == len(want)
+        for q, w in zip(seqs, want):
+            assert [int(csr.dpids[x]) for x in q] == [x for x, _ in w]
+
+
+def test_shortest_fullsize_fat_tree(ctx):
+    fabric = T.fat_tree(48)
+    csr = fabric.csr()
+    dsts = np.unique(fabric.host_table()[0]).astype(np.int32)
+    ctx.upload(csr)
+    dist, nh, nhp = ctx.shortest_tables(dsts)
+    do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
+    np.testing.assert_array_equal(dist, do)
+    np.testing.assert_array_equal(nh, nho)
+    np.testing.assert_array_equal(nhp, nhpo)
+
+
+def test_shortest_global_path_torus(ctx):
+    """V > 6400 -> masks in HBM, one launch per level."""
+    fabric = T.torus3d(24, 24, 16)
+    csr = fabric.csr()
+    dsts = np.linspace(0, csr.V - 1, 130).astype(np.int32)
+    ctx.upload(csr)
+    dist, nh, nhp = ctx.shortest_tables(dsts)
+    do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
+    np.testing.assert_array_equal(dist, do)
+    np.testing.assert_array_equal(nh, nho)
+    np.testing.assert_array_equal(nhp, nhpo)
+
+
+@pytest.mark.parametrize("name", ["mock", "fat_tree_k8", "dragonfly_a4_h2_p2",
+                                  "random_V60_dense", "torus_5x3x2"])
+def test_apsp_small(ctx, name):
+    csr = G.Golden(name).fabric().csr()
+    ctx.upload(csr)
+    np.testing.assert_array_equal(ctx.apsp(), O.apsp(csr))
+
+
+def test_apsp_matches_msbfs_dragonfly(ctx):
+    csr = T.dragonfly(16, 8, 8).csr()
+    ctx.upload(csr)
+    D = ctx.apsp()
+    dist, _, _ = ctx.shortest_tables(np.arange(csr.V, dtype=np.int32), with_nexthop=False)
+    np.testing.assert_array_equal(D.T, dist)
+
+
+def test_device_pointer_path_matches_host_path(ctx):
+    torch = pytest.importorskip("torch")
+    csr = T.fat_tree(16).csr()
+    ctx.upload(csr)
+    srcs = np.arange(csr.V, dtype=np.int32)
+    p, t, h = ctx.dfs_tables(srcs)
+    dev = torch.device("cuda", 0)
+    ts = torch.from_numpy(srcs).to(dev)
+    tp = torch.empty((len(srcs), csr.V), dtype=torch.int32, device=dev)
+    tt = torch.empty_like(tp)
+    th = torch.empty_like(tp)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    ctx.dfs_tables_device(ts.data_ptr(), len(srcs), tp.data_ptr(), tt.data_ptr(),
+                          th.data_ptr(), timing=True)
+    ms = ctx.last_kernel_ms()
+    torch.cuda.synchronize()
+    ctx.set_stream(None)
+    assert ms > 0
+    np.testing.assert_array_equal(tp.cpu().numpy(), p)
+    np.testing.assert_array_equal(tt.cpu().numpy(), t)
+    np.testing.assert_array_equal(th.cpu().numpy(), h)
+
+
+def test_out_of_range_source_rows_device(ctx):
+    torch = pytest.importorskip("torch")
+    csr = T.fat_tree(4).csr()
+    ctx.upload(csr)
+    dev = torch.device("cuda", 0)
+    ts = torch.tensor([-1, 3, csr.V + 5], dtype=torch.int32, device=dev)
+    tp = torch.empty((3, csr.V), dtype=torch.int32, device=dev)
+    tt = torch.empty_like(tp)
+    ctx.dfs_tables_device(ts.data_ptr(), 3, tp.data_ptr(), tt.data_ptr())
+    ctx.synchronize()
+    p = tp.cpu().numpy()
+    assert (p[0] == -1).all() and (p[2] == -1).all() and p[1, 3] == 3
+
+
+def test_host_path_rejects_bad_source(ctx):
+    ctx.upload(T.fat_tree(4).csr())
+    with pytest.raises(_native.SdnrError) as ei:
+        ctx.dfs_tables(np.array([0, 999], np.int32))
+    assert ei.value.code == -22
+
+
+def test_upload_rejects_unsorted_rows(ctx):
+    from sdnmpi_amd.topologies import CSR
+    bad = CSR(np.array([1, 2, 3]), np.array([0, 2, 2, 2]), np.array([2, 1]), np.array([1, 2]))
+    with pytest.raises(_native.SdnrError):
+        ctx.upload(bad)
+
+
+def test_edge_graphs(ctx):
+    from sdnmpi_amd.topologies import CSR
+    # isolated vertices only
+    c = CSR(np.array([4, 9]), np.array([0, 0, 0]), np.zeros(0, np.int32), np.zeros(0, np.int32))
+    ctx.upload(c)
+    p, t, h = ctx.dfs_tables(np.array([0, 1], np.int32))
+    np.testing.assert_array_equal(p, [[0, -1], [-1, 1]])
+    np.testing.assert_array_equal(h, [[0, -1], [-1, 0]])
+    dist, nh, nhp = ctx.shortest_tables(np.array([1], np.int32))
+    np.testing.assert_array_equal(dist, [[0xFFFF, 0]])
+    # a star with 130 leaves: rows wider than one wavefront (CSR chunks)
+    V = 131
+    rp = np.zeros(V + 1, np.int64)
+    rp[1] = V - 1
+    rp[2:] = V - 1 + np.arange(1, V)
+    col = np.concatenate([np.arange(1, V), np.zeros(V - 1, np.int64)])
+    port = np.arange(len(col))
+    star = CSR(np.arange(1, V + 1), rp, col, port)
+    _check_dfs(ctx, star, np.arange(V, dtype=np.int32))
