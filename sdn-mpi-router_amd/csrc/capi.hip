@@ -64,10 +64,16 @@ static void free_graph(sdnr_ctx *c)
     c->max_deg = 0;
 }
 
-static int upload(int32_t **dst, const void *src, size_t bytes, hipStream_t s)
+static constexpr size_t kPad = SDNR_WAVE;
+
+// device copy of `bytes` plus `pad` int32 entries of -1 behind them
+static int upload(int32_t **dst, const void *src, size_t bytes, size_t pad, hipStream_t s)
 {
-    SDNR_HIP(hipMalloc(reinterpret_cast<void **>(dst), bytes < 4 ? 4 : bytes));
+    const size_t total = bytes + pad * sizeof(int32_t);
+    SDNR_HIP(hipMalloc(reinterpret_cast<void **>(dst), total < 4 ? 4 : total));
     if (bytes) SDNR_HIP(hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, s));
+    if (pad) SDNR_HIP(hipMemsetAsync(reinterpret_cast<char *>(*dst) + bytes, 0xFF,
+                                     pad * sizeof(int32_t), s));
     return SDNR_OK;
 }
 
@@ -179,9 +185,11 @@ int sdnr_graph_upload(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_pt
     SDNR_HIP(hipStreamSynchronize(ctx->stream));
     free_graph(ctx);
     int rc;
-    if ((rc = upload(&ctx->row_ptr, row_ptr, sizeof(int32_t) * ((size_t)V + 1), ctx->stream)) ||
-        (rc = upload(&ctx->col, col, sizeof(int32_t) * (size_t)E, ctx->stream)) ||
-        (rc = upload(&ctx->port, port, sizeof(int32_t) * (size_t)E, ctx->stream))) {
+    // adjacency arrays carry kPad trailing entries so a wavefront may load a
+    // whole 64-lane window past the last row unconditionally
+    if ((rc = upload(&ctx->row_ptr, row_ptr, sizeof(int32_t) * ((size_t)V + 1), 0, ctx->stream)) ||
+        (rc = upload(&ctx->col, col, sizeof(int32_t) * (size_t)E, kPad, ctx->stream)) ||
+        (rc = upload(&ctx->port, port, sizeof(int32_t) * (size_t)E, kPad, ctx->stream))) {
         free_graph(ctx);
         return rc;
     }
@@ -199,8 +207,8 @@ int sdnr_graph_upload(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_pt
                 ec[(size_t)u * W + (e - row_ptr[u])] = col[e];
                 ep[(size_t)u * W + (e - row_ptr[u])] = port[e];
             }
-        if ((rc = upload(&ctx->ell_col, ec.data(), ec.size() * 4, ctx->stream)) ||
-            (rc = upload(&ctx->ell_port, ep.data(), ep.size() * 4, ctx->stream))) {
+        if ((rc = upload(&ctx->ell_col, ec.data(), ec.size() * 4, kPad, ctx->stream)) ||
+            (rc = upload(&ctx->ell_port, ep.data(), ep.size() * 4, kPad, ctx->stream))) {
             free_graph(ctx);
             return rc;
         }

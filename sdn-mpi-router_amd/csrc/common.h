@@ -57,6 +57,15 @@ struct sdnr_ctx {
     bool timed = false;
 };
 
+// Raise a kernel's dynamic-LDS limit; a refusal (e.g. static LDS + bytes >
+// 160 KiB) is cleared so it cannot surface later as hipGetLastError().
+inline void sdnr_allow_lds(const void *fn, size_t bytes)
+{
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) !=
+        hipSuccess)
+        (void)hipGetLastError();
+}
+
 // error plumbing (capi.hip)
 int sdnr_fail(int code, const char *fmt, ...);
 int sdnr_hip_fail(hipError_t e, const char *what);

@@ -34,7 +34,7 @@ namespace {
 constexpr int kRing = 1024;   // LDS stack ring entries (global mode)
 
 template <bool ELL, bool HOPS>
-__global__ __launch_bounds__(64) void dfs_lds_kernel(
+__global__ __launch_bounds__(64) void dfs_lds_wide_kernel(
     int V, int W, const int32_t *__restrict__ row_ptr,
     const int32_t *__restrict__ col, const int32_t *__restrict__ port,
     const int32_t *__restrict__ src, int nsrc, int32_t *__restrict__ out_parent,
@@ -141,7 +141,7 @@ __global__ __launch_bounds__(64) void dfs_lds_kernel(
 }
 
 template <bool ELL, bool HOPS>
-__global__ __launch_bounds__(64) void dfs_global_kernel(
+__global__ __launch_bounds__(64) void dfs_global_wide_kernel(
     int V, int W, const int32_t *__restrict__ row_ptr,
     const int32_t *__restrict__ col, const int32_t *__restrict__ port,
     const int32_t *__restrict__ src, int nsrc, int32_t *__restrict__ out_parent,
@@ -261,20 +261,303 @@ __global__ __launch_bounds__(64) void dfs_global_kernel(
     }
 }
 
-template <typename K>
-void allow_full_lds(K kernel)
+// ---------------------------------------------------------------------------
+// Batched pops.  A pop that finds no unvisited neighbour (a "leaf" pop)
+// changes nothing -- no mark, no push -- so a run of leaf pops can be checked
+// against the same visited set in any order.  The batched kernels read the
+// top K stack entries, issue the K row loads and then the K visited gathers
+// back to back (one memory latency for K pops instead of K), and take the
+// first entry from the top that has an unvisited neighbour: everything above
+// it was a leaf pop, it is processed exactly as the sequential search would,
+// and everything below stays on the stack for the next batch (its check is
+// stale).  On the k=48 fat-tree 96% of pops are leaves.
+//
+// Rows must fit one wavefront (max out-degree <= 64): ELL rows at u*W, or
+// CSR rows (row_ptr loads issued with the batch).  Adjacency arrays carry 64
+// padding entries so every lane may load unconditionally (a guarded load per
+// batch slot makes hipcc wait vmcnt(0) per slot).
+// ---------------------------------------------------------------------------
+
+template <bool ELL, int K>
+__device__ __forceinline__ void batch_rows(int kk, const int (&uu)[K], int W,
+                                           const int32_t *__restrict__ row_ptr,
+                                           const int32_t *__restrict__ col,
+                                           int (&rs)[K], int (&v)[K])
 {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              SDNR_MAX_LDS_PER_BLOCK);
+    const int lane = lane_id();
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const int u = uu[i];
+        int a, b;
+        if (ELL) {
+            a = u * W;
+            b = a + W;
+        } else {
+            a = row_ptr[u];
+            b = row_ptr[u + 1];
+        }
+        rs[i] = a;
+        const int x = col[a + lane];
+        v[i] = (i < kk && a + lane < b) ? x : -1;
+    }
+}
+
+template <int K>
+__device__ __forceinline__ int first_live(const uint64_t (&m)[K])
+{
+    int istar = K;
+#pragma unroll
+    for (int i = K - 1; i >= 0; --i)
+        if (m[i] != 0) istar = i;
+    return istar;
+}
+
+// small graphs (V < 65536): all per-source state in LDS, tables flushed once
+template <bool ELL, bool HOPS, int K>
+__global__ __launch_bounds__(64) void dfs_lds_batch_kernel(
+    int V, int W, const int32_t *__restrict__ row_ptr,
+    const int32_t *__restrict__ col, const int32_t *__restrict__ port,
+    const int32_t *__restrict__ src, int nsrc, int32_t *__restrict__ out_parent,
+    int32_t *__restrict__ out_port, int32_t *__restrict__ out_hops)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int VW = (V + 31) >> 5;
+    const int VWp = (VW + 3) & ~3;
+    uint32_t *vis = lds;                       // visited bits
+    uint32_t *stk = vis + VWp;                 // stack: v | depth << 16
+    uint32_t *ps = stk + V;                    // parent | row slot << 16
+    uint16_t *dep = reinterpret_cast<uint16_t *>(ps + V);
+    const int lane = lane_id();
+
+    for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
+        const int s = uniform(src[si]);
+        int32_t *prow = out_parent + (size_t)si * V;
+        int32_t *trow = out_port + (size_t)si * V;
+        int32_t *hrow = HOPS ? out_hops + (size_t)si * V : nullptr;
+        if (s < 0 || s >= V) {
+            for (int v = lane; v < V; v += SDNR_WAVE) {
+                prow[v] = -1;
+                trow[v] = -1;
+                if (HOPS) hrow[v] = -1;
+            }
+            continue;
+        }
+        for (int w = lane; w < VW; w += SDNR_WAVE) vis[w] = 0u;
+        __syncthreads();
+        if (lane == 0) {
+            vis[s >> 5] = 1u << (s & 31);
+            ps[s] = (uint32_t)s;
+            dep[s] = 0;
+            stk[0] = (uint32_t)s;
+        }
+        __syncthreads();
+
+        int sp = 1;
+        while (sp > 0) {
+            const int kk = sp < K ? sp : K;
+            const uint32_t mine = lane < kk ? stk[sp - 1 - lane] : 0u;
+            uint32_t ent[K];
+            int uu[K];
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                ent[i] = (uint32_t)read_lane((int)mine, i);
+                uu[i] = (int)(ent[i] & 0xFFFFu);
+            }
+            int rs[K], v[K];
+            batch_rows<ELL, K>(kk, uu, W, row_ptr, col, rs, v);
+            uint64_t m[K];
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const int vi = v[i] < 0 ? 0 : v[i];
+                const uint32_t w = vis[vi >> 5];
+                m[i] = __ballot(v[i] >= 0 && ((w >> (vi & 31)) & 1u) == 0u);
+            }
+            const int istar = first_live<K>(m);
+            if (istar == K) {                      // kk leaf pops
+                sp -= kk;
+                continue;
+            }
+            sp -= istar + 1;
+            uint64_t mm = 0;
+            int vv = -1;
+            uint32_t eu = 0;
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                if (i == istar) {
+                    mm = m[i];
+                    vv = v[i];
+                    eu = ent[i];
+                }
+            const int u = (int)(eu & 0xFFFFu);
+            const int du = (int)(eu >> 16);
+            if ((mm >> lane) & 1ull) {
+                const int rank = lanes_below(mm);
+                atomicOr(&vis[vv >> 5], 1u << (vv & 31));
+                ps[vv] = (uint32_t)u | ((uint32_t)lane << 16);
+                if (HOPS) dep[vv] = (uint16_t)(du + 1);
+                stk[sp + rank] = (uint32_t)vv | ((uint32_t)(du + 1) << 16);
+            }
+            sp += __popcll(mm);
+        }
+        __syncthreads();
+
+        for (int v = lane; v < V; v += SDNR_WAVE) {
+            int p = -1, pt = -1, h = -1;
+            if ((vis[v >> 5] >> (v & 31)) & 1u) {
+                const uint32_t x = ps[v];
+                p = (int)(x & 0xFFFFu);
+                if (v == s) {
+                    h = 0;
+                } else {
+                    const int slot = (int)(x >> 16);
+                    pt = ELL ? port[(size_t)p * W + slot] : port[row_ptr[p] + slot];
+                    h = HOPS ? (int)dep[v] : 0;
+                }
+            }
+            prow[v] = p;
+            trow[v] = pt;
+            if (HOPS) hrow[v] = h;
+        }
+        __syncthreads();
+    }
+}
+
+// large graphs: visited bits + a stack ring in LDS (spilled to HBM in
+// halves), table entries stored as vertices are pushed
+template <bool ELL, bool HOPS, int K>
+__global__ __launch_bounds__(64) void dfs_global_batch_kernel(
+    int V, int W, const int32_t *__restrict__ row_ptr,
+    const int32_t *__restrict__ col, const int32_t *__restrict__ port,
+    const int32_t *__restrict__ src, int nsrc, int32_t *__restrict__ out_parent,
+    int32_t *__restrict__ out_port, int32_t *__restrict__ out_hops,
+    uint2 *__restrict__ spill_all)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int VW = (V + 31) >> 5;
+    const int VWp = (VW + 3) & ~3;
+    uint32_t *vis = lds;
+    uint2 *ring = reinterpret_cast<uint2 *>(vis + VWp);   // (v, depth)
+    uint2 *spill = spill_all + (size_t)blockIdx.x * (size_t)V;
+    const int lane = lane_id();
+
+    for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
+        const int s = uniform(src[si]);
+        int32_t *prow = out_parent + (size_t)si * V;
+        int32_t *trow = out_port + (size_t)si * V;
+        int32_t *hrow = HOPS ? out_hops + (size_t)si * V : nullptr;
+        if (s < 0 || s >= V) {
+            for (int v = lane; v < V; v += SDNR_WAVE) {
+                prow[v] = -1;
+                trow[v] = -1;
+                if (HOPS) hrow[v] = -1;
+            }
+            continue;
+        }
+        for (int w = lane; w < VW; w += SDNR_WAVE) vis[w] = 0u;
+        __syncthreads();
+        if (lane == 0) {
+            vis[s >> 5] = 1u << (s & 31);
+            prow[s] = s;
+            trow[s] = -1;
+            if (HOPS) hrow[s] = 0;
+            ring[0] = make_uint2((uint32_t)s, 0u);
+        }
+        __syncthreads();
+
+        int lsp = 1, bot = 0, gsp = 0;        // ring depth, ring bottom, spilled
+        for (;;) {
+            if (lsp == 0) {
+                if (gsp == 0) break;
+                const int n = gsp < kRing / 2 ? gsp : kRing / 2;
+                // the spill was written by this wave: wait for the stores and
+                // drop this CU's L1 copy before reading it back
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                bot = (bot - n) & (kRing - 1);
+                for (int i = lane; i < n; i += SDNR_WAVE)
+                    ring[(bot + i) & (kRing - 1)] = spill[gsp - n + i];
+                gsp -= n;
+                lsp = n;
+            }
+            const int kk = lsp < K ? lsp : K;
+            uint2 me = make_uint2(0u, 0u);
+            if (lane < kk) me = ring[(bot + lsp - 1 - lane) & (kRing - 1)];
+            uint32_t ent[K], edep[K];
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                ent[i] = (uint32_t)read_lane((int)me.x, i);
+                edep[i] = (uint32_t)read_lane((int)me.y, i);
+            }
+            int uu[K];
+#pragma unroll
+            for (int i = 0; i < K; ++i) uu[i] = (int)ent[i];
+            int rs[K], v[K];
+            batch_rows<ELL, K>(kk, uu, W, row_ptr, col, rs, v);
+            uint64_t m[K];
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const int vi = v[i] < 0 ? 0 : v[i];
+                const uint32_t w = vis[vi >> 5];
+                m[i] = __ballot(v[i] >= 0 && ((w >> (vi & 31)) & 1u) == 0u);
+            }
+            const int istar = first_live<K>(m);
+            if (istar == K) {
+                lsp -= kk;
+                continue;
+            }
+            lsp -= istar + 1;
+            uint64_t mm = 0;
+            int vv = -1, r0 = 0;
+            uint32_t eu = 0, ed = 0;
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                if (i == istar) {
+                    mm = m[i];
+                    vv = v[i];
+                    eu = ent[i];
+                    ed = edep[i];
+                    r0 = rs[i];
+                }
+            const int cnt = __popcll(mm);
+            if (lsp + cnt > kRing) {               // spill the oldest half
+                for (int i = lane; i < kRing / 2; i += SDNR_WAVE)
+                    spill[gsp + i] = ring[(bot + i) & (kRing - 1)];
+                gsp += kRing / 2;
+                bot = (bot + kRing / 2) & (kRing - 1);
+                lsp -= kRing / 2;
+            }
+            if ((mm >> lane) & 1ull) {
+                const int rank = lanes_below(mm);
+                atomicOr(&vis[vv >> 5], 1u << (vv & 31));
+                prow[vv] = (int)eu;
+                trow[vv] = port[r0 + lane];
+                if (HOPS) hrow[vv] = (int)ed + 1;
+                ring[(bot + lsp + rank) & (kRing - 1)] = make_uint2((uint32_t)vv, ed + 1u);
+            }
+            lsp += cnt;
+        }
+        __syncthreads();
+        for (int v = lane; v < V; v += SDNR_WAVE) {
+            if (((vis[v >> 5] >> (v & 31)) & 1u) == 0u) {
+                prow[v] = -1;
+                trow[v] = -1;
+                if (HOPS) hrow[v] = -1;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <typename Kern>
+void allow_full_lds(Kern kernel)
+{
+    sdnr_allow_lds(reinterpret_cast<const void *>(kernel), SDNR_MAX_LDS_PER_BLOCK);
 }
 
 size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 }  // namespace
 
-// LDS bytes per source of the two strategies (also used by the host-side
-// planner through sdnr_launch_dfs)
+// LDS bytes per source of the two strategies
 static size_t dfs_lds_bytes_small(int V)
 {
     const size_t VWp = (size_t)((((V + 31) >> 5) + 3) & ~3);
@@ -287,6 +570,70 @@ static size_t dfs_lds_bytes_global(int V)
     return align16(4 * VWp + 8 * (size_t)kRing);
 }
 
+namespace {
+
+struct DfsArgs {
+    int V, W;
+    const int32_t *row_ptr, *col, *port, *src;
+    int nsrc;
+    int32_t *parent, *port_out, *hops;
+    uint2 *spill;
+};
+
+template <bool ELL, bool HOPS, int K>
+void launch_batch(bool small, int grid, size_t lds, hipStream_t st, const DfsArgs &a)
+{
+    if (small) {
+        auto k = dfs_lds_batch_kernel<ELL, HOPS, K>;
+        allow_full_lds(k);
+        hipLaunchKernelGGL(k, dim3(grid), dim3(64), lds, st, a.V, a.W, a.row_ptr, a.col, a.port,
+                           a.src, a.nsrc, a.parent, a.port_out, a.hops);
+    } else {
+        auto k = dfs_global_batch_kernel<ELL, HOPS, K>;
+        allow_full_lds(k);
+        hipLaunchKernelGGL(k, dim3(grid), dim3(64), lds, st, a.V, a.W, a.row_ptr, a.col, a.port,
+                           a.src, a.nsrc, a.parent, a.port_out, a.hops, a.spill);
+    }
+}
+
+template <bool ELL, bool HOPS>
+void launch_batch_k(int K, bool small, int grid, size_t lds, hipStream_t st, const DfsArgs &a)
+{
+    if (K >= 16) launch_batch<ELL, HOPS, 16>(small, grid, lds, st, a);
+    else if (K >= 8) launch_batch<ELL, HOPS, 8>(small, grid, lds, st, a);
+    else if (K >= 4) launch_batch<ELL, HOPS, 4>(small, grid, lds, st, a);
+    else launch_batch<ELL, HOPS, 1>(small, grid, lds, st, a);
+}
+
+template <bool HOPS>
+void launch_wide(bool small, int grid, size_t lds, hipStream_t st, const DfsArgs &a)
+{
+    if (small) {
+        auto k = dfs_lds_wide_kernel<false, HOPS>;
+        allow_full_lds(k);
+        hipLaunchKernelGGL(k, dim3(grid), dim3(64), lds, st, a.V, a.W, a.row_ptr, a.col, a.port,
+                           a.src, a.nsrc, a.parent, a.port_out, a.hops);
+    } else {
+        auto k = dfs_global_wide_kernel<false, HOPS>;
+        allow_full_lds(k);
+        hipLaunchKernelGGL(k, dim3(grid), dim3(64), lds, st, a.V, a.W, a.row_ptr, a.col, a.port,
+                           a.src, a.nsrc, a.parent, a.port_out, a.hops, a.spill);
+    }
+}
+
+}  // namespace
+
+// pops checked per batch: wide rows make each leaf pop expensive, so batch
+// deeper; SDNROUTE_DFS_BATCH=1|4|8|16 overrides (tuning / tests)
+static int dfs_batch_depth(const sdnr_ctx *ctx)
+{
+    if (const char *f = getenv("SDNROUTE_DFS_BATCH")) {
+        const int k = atoi(f);
+        if (k == 1 || k == 4 || k == 8 || k == 16) return k;
+    }
+    return ctx->max_deg >= 12 ? 16 : 8;
+}
+
 int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
                     int32_t *d_parent, int32_t *d_port, int32_t *d_hops)
 {
@@ -294,7 +641,7 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
     if (nsrc == 0 || V == 0) return SDNR_OK;
     const bool ell = ctx->W > 0;
     const bool hops = d_hops != nullptr;
-    const int W = ctx->W;
+    const bool narrow = ctx->max_deg <= SDNR_WAVE;     // one row = one wavefront
     const size_t small_b = dfs_lds_bytes_small(V);
     const size_t cu_blocks_small = SDNR_LDS_PER_CU / small_b;
     bool small = V < 65536 && small_b <= 64 * 1024 &&
@@ -305,53 +652,33 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         if (!strcmp(f, "global")) small = false;
         else if (!strcmp(f, "lds") && V < 65536 && small_b <= SDNR_MAX_LDS_PER_BLOCK) small = true;
     }
-    if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
-    if (small) {
-        size_t bpc = cu_blocks_small < 16 ? cu_blocks_small : 16;
-        if (bpc < 1) bpc = 1;
-        int grid = (int)((size_t)ctx->num_cus * bpc);
-        if (grid > nsrc) grid = nsrc;
-#define SDNR_DFS_SMALL(E_, H_)                                                    \
-    do {                                                                          \
-        auto k = dfs_lds_kernel<E_, H_>;                                          \
-        allow_full_lds(k);                                                        \
-        hipLaunchKernelGGL(k, dim3(grid), dim3(64), small_b, ctx->stream, V, W,   \
-                           ctx->row_ptr, E_ ? ctx->ell_col : ctx->col,            \
-                           E_ ? ctx->ell_port : ctx->port, d_src, nsrc, d_parent, \
-                           d_port, d_hops);                                       \
-    } while (0)
-        if (ell && hops) SDNR_DFS_SMALL(true, true);
-        else if (ell) SDNR_DFS_SMALL(true, false);
-        else if (hops) SDNR_DFS_SMALL(false, true);
-        else SDNR_DFS_SMALL(false, false);
-#undef SDNR_DFS_SMALL
-    } else {
-        const size_t gb = dfs_lds_bytes_global(V);
-        if (gb > SDNR_MAX_LDS_PER_BLOCK)
-            return sdnr_fail(SDNR_ERR_INVAL, "graph too large for the LDS visited set (V=%d)", V);
-        size_t bpc = SDNR_LDS_PER_CU / gb;
-        if (bpc > 16) bpc = 16;
-        if (bpc < 1) bpc = 1;
-        int grid = (int)((size_t)ctx->num_cus * bpc);
-        if (grid > nsrc) grid = nsrc;
+    size_t lds = small ? small_b : dfs_lds_bytes_global(V);
+    if (lds > SDNR_MAX_LDS_PER_BLOCK)
+        return sdnr_fail(SDNR_ERR_INVAL, "graph too large for the LDS visited set (V=%d)", V);
+    size_t bpc = SDNR_LDS_PER_CU / lds;
+    if (bpc > 16) bpc = 16;
+    if (bpc < 1) bpc = 1;
+    int grid = (int)((size_t)ctx->num_cus * bpc);
+    if (grid > nsrc) grid = nsrc;
+    uint2 *spill = nullptr;
+    if (!small) {
         const size_t need = (size_t)grid * (size_t)V * sizeof(uint2);
         int rc = sdnr_reserve(&ctx->scratch, &ctx->scratch_bytes, need);
         if (rc) return rc;
-        uint2 *spill = static_cast<uint2 *>(ctx->scratch);
-#define SDNR_DFS_GLOBAL(E_, H_)                                                   \
-    do {                                                                          \
-        auto k = dfs_global_kernel<E_, H_>;                                       \
-        allow_full_lds(k);                                                        \
-        hipLaunchKernelGGL(k, dim3(grid), dim3(64), gb, ctx->stream, V, W,        \
-                           ctx->row_ptr, E_ ? ctx->ell_col : ctx->col,            \
-                           E_ ? ctx->ell_port : ctx->port, d_src, nsrc, d_parent, \
-                           d_port, d_hops, spill);                                \
-    } while (0)
-        if (ell && hops) SDNR_DFS_GLOBAL(true, true);
-        else if (ell) SDNR_DFS_GLOBAL(true, false);
-        else if (hops) SDNR_DFS_GLOBAL(false, true);
-        else SDNR_DFS_GLOBAL(false, false);
-#undef SDNR_DFS_GLOBAL
+        spill = static_cast<uint2 *>(ctx->scratch);
+    }
+    DfsArgs a{V, ctx->W, ctx->row_ptr, ell ? ctx->ell_col : ctx->col,
+              ell ? ctx->ell_port : ctx->port, d_src, nsrc, d_parent, d_port, d_hops, spill};
+    if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
+    if (narrow) {
+        const int K = dfs_batch_depth(ctx);
+        if (ell && hops) launch_batch_k<true, true>(K, small, grid, lds, ctx->stream, a);
+        else if (ell) launch_batch_k<true, false>(K, small, grid, lds, ctx->stream, a);
+        else if (hops) launch_batch_k<false, true>(K, small, grid, lds, ctx->stream, a);
+        else launch_batch_k<false, false>(K, small, grid, lds, ctx->stream, a);
+    } else {
+        if (hops) launch_wide<true>(small, grid, lds, ctx->stream, a);
+        else launch_wide<false>(small, grid, lds, ctx->stream, a);
     }
     SDNR_HIP(hipGetLastError());
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));

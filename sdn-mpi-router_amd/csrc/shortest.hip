@@ -166,9 +166,7 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
     const size_t lds = (size_t)V * 3 * sizeof(uint64_t);
     if (lds <= 150 * 1024) {
         auto k = msbfs_lds_kernel;
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  SDNR_MAX_LDS_PER_BLOCK);
+        if (lds > 64 * 1024) sdnr_allow_lds(reinterpret_cast<const void *>(k), lds);
         hipLaunchKernelGGL(k, dim3(nbatch), dim3(kBfsThreads), lds, ctx->stream, V,
                            ctx->row_ptr, ctx->col, d_dst, ndst, d_dist);
         SDNR_HIP(hipGetLastError());
