@@ -58,6 +58,8 @@ static void free_graph(sdnr_ctx *c)
         if (*b) (void)hipFree(*b);
         *b = nullptr;
     }
+    if (c->adj16) (void)hipFree(c->adj16);
+    c->adj16 = nullptr;
     c->V = -1;
     c->E = 0;
     c->W = 0;
@@ -213,9 +215,25 @@ int sdnr_graph_upload(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_pt
             return rc;
         }
         SDNR_HIP(hipStreamSynchronize(ctx->stream));   // before ec/ep go away
-    } else {
-        SDNR_HIP(hipStreamSynchronize(ctx->stream));
     }
+    // u16 rows of stride 64 (one 128-byte line) for the cooperative DFS:
+    // padding and the extra row V hold the sentinel vertex V
+    if (V < 65535 && maxdeg <= SDNR_WAVE) {
+        std::vector<uint16_t> a16(((size_t)V + 1) * SDNR_WAVE, (uint16_t)V);
+        for (int32_t u = 0; u < V; ++u)
+            for (int32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e)
+                a16[(size_t)u * SDNR_WAVE + (e - row_ptr[u])] = (uint16_t)col[e];
+        const size_t bytes = a16.size() * sizeof(uint16_t);
+        hipError_t he = hipMalloc(reinterpret_cast<void **>(&ctx->adj16), bytes);
+        if (he == hipSuccess)
+            he = hipMemcpyAsync(ctx->adj16, a16.data(), bytes, hipMemcpyHostToDevice, ctx->stream);
+        if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
+        if (he != hipSuccess) {
+            free_graph(ctx);
+            return sdnr_hip_fail(he, "graph_upload(adj16)");
+        }
+    }
+    SDNR_HIP(hipStreamSynchronize(ctx->stream));
     ctx->V = V;
     ctx->E = E;
     ctx->W = W;

@@ -45,6 +45,7 @@ struct sdnr_ctx {
     int32_t W = 0;                      // ELL row width (0: CSR only)
     int32_t *row_ptr = nullptr, *col = nullptr, *port = nullptr;
     int32_t *ell_col = nullptr, *ell_port = nullptr;
+    uint16_t *adj16 = nullptr;          // (V+1) rows x 64 u16, sentinel V (V < 65535)
 
     // grow-only device scratch / staging
     void *scratch = nullptr;

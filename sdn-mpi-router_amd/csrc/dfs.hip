@@ -284,21 +284,42 @@ __device__ __forceinline__ void batch_rows(int kk, const int (&uu)[K], int W,
                                            const int32_t *__restrict__ col,
                                            int (&rs)[K], int (&v)[K])
 {
+    // every slot loads unconditionally (addresses stay inside the padded
+    // arrays); validity is applied afterwards with bit masks, never with a
+    // branch, so the K loads are all in flight together
     const int lane = lane_id();
+    int x[K], b[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
         const int u = uu[i];
-        int a, b;
         if (ELL) {
-            a = u * W;
-            b = a + W;
+            rs[i] = u * W;
+            b[i] = rs[i] + W;
         } else {
-            a = row_ptr[u];
-            b = row_ptr[u + 1];
+            rs[i] = row_ptr[u];
+            b[i] = row_ptr[u + 1];
         }
-        rs[i] = a;
-        const int x = col[a + lane];
-        v[i] = (i < kk && a + lane < b) ? x : -1;
+        x[i] = col[rs[i] + lane];
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const int ok = -(int)((i < kk) & (rs[i] + lane < b[i]));   // 0 or -1
+        v[i] = (x[i] & ok) | ~ok;
+    }
+}
+
+// visited test of K candidate rows: K independent LDS gathers, then ballots
+template <int K>
+__device__ __forceinline__ void batch_unvisited(const uint32_t *vis, const int (&v)[K],
+                                                uint64_t (&m)[K])
+{
+    uint32_t w[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) w[i] = vis[(v[i] & 0x7FFFFFFF) >> 5 & ((v[i] >> 31) ^ -1)];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const bool fresh = (v[i] >= 0) & (((w[i] >> (v[i] & 31)) & 1u) == 0u);
+        m[i] = __ballot(fresh);
     }
 }
 
@@ -355,7 +376,9 @@ __global__ __launch_bounds__(64) void dfs_lds_batch_kernel(
         int sp = 1;
         while (sp > 0) {
             const int kk = sp < K ? sp : K;
-            const uint32_t mine = lane < kk ? stk[sp - 1 - lane] : 0u;
+            const int slot = sp - 1 - lane;
+            uint32_t mine = stk[slot < 0 ? 0 : slot];
+            mine = lane < kk ? mine : 0u;            // slots past the stack: vertex 0
             uint32_t ent[K];
             int uu[K];
 #pragma unroll
@@ -366,12 +389,7 @@ __global__ __launch_bounds__(64) void dfs_lds_batch_kernel(
             int rs[K], v[K];
             batch_rows<ELL, K>(kk, uu, W, row_ptr, col, rs, v);
             uint64_t m[K];
-#pragma unroll
-            for (int i = 0; i < K; ++i) {
-                const int vi = v[i] < 0 ? 0 : v[i];
-                const uint32_t w = vis[vi >> 5];
-                m[i] = __ballot(v[i] >= 0 && ((w >> (vi & 31)) & 1u) == 0u);
-            }
+            batch_unvisited<K>(vis, v, m);
             const int istar = first_live<K>(m);
             if (istar == K) {                      // kk leaf pops
                 sp -= kk;
@@ -479,8 +497,9 @@ __global__ __launch_bounds__(64) void dfs_global_batch_kernel(
                 lsp = n;
             }
             const int kk = lsp < K ? lsp : K;
-            uint2 me = make_uint2(0u, 0u);
-            if (lane < kk) me = ring[(bot + lsp - 1 - lane) & (kRing - 1)];
+            uint2 me = ring[(bot + lsp - 1 - lane) & (kRing - 1)];
+            me.x = lane < kk ? me.x : 0u;            // slots past the stack: vertex 0
+            me.y = lane < kk ? me.y : 0u;
             uint32_t ent[K], edep[K];
 #pragma unroll
             for (int i = 0; i < K; ++i) {
@@ -493,12 +512,7 @@ __global__ __launch_bounds__(64) void dfs_global_batch_kernel(
             int rs[K], v[K];
             batch_rows<ELL, K>(kk, uu, W, row_ptr, col, rs, v);
             uint64_t m[K];
-#pragma unroll
-            for (int i = 0; i < K; ++i) {
-                const int vi = v[i] < 0 ? 0 : v[i];
-                const uint32_t w = vis[vi >> 5];
-                m[i] = __ballot(v[i] >= 0 && ((w >> (vi & 31)) & 1u) == 0u);
-            }
+            batch_unvisited<K>(vis, v, m);
             const int istar = first_live<K>(m);
             if (istar == K) {
                 lsp -= kk;
@@ -547,6 +561,152 @@ __global__ __launch_bounds__(64) void dfs_global_batch_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Cooperative batched pops (small graphs, the k=48 headline path).
+//
+// With one wavefront per source the batched loop is instruction-issue bound
+// (one wave per SIMD pays >= 4 cycles per instruction on the chain).  Here a
+// workgroup of NW waves owns one source: each wave checks KW of the K = NW*KW
+// top stack entries (row load + visited gather + ballot), publishes one flag
+// word per wave, and after one barrier every wave derives the same first
+// live slot; the owning wave pushes, and a second barrier publishes the push
+// (skipped when all K entries were leaf pops).  Rows are u16 with stride 64
+// (one 128-byte line each) padded with a sentinel vertex V whose visited bit
+// is always set, and row V is all sentinel: no lane or slot needs a validity
+// mask.  Every wave keeps its own copy of the stack depth; all copies follow
+// the same deterministic updates.
+// ---------------------------------------------------------------------------
+template <int NW, int KW, bool HOPS>
+__global__ __launch_bounds__(NW * 64) void dfs_coop_kernel(
+    int V, const uint16_t *__restrict__ adj, const int32_t *__restrict__ row_ptr,
+    const int32_t *__restrict__ port, const int32_t *__restrict__ src, int nsrc,
+    int32_t *__restrict__ out_parent, int32_t *__restrict__ out_port,
+    int32_t *__restrict__ out_hops)
+{
+    constexpr int K = NW * KW;
+    static_assert(K <= 64, "one flag bit per slot");
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int VW = (V + 1 + 31) >> 5;            // + sentinel bit V
+    const int VWp = (VW + 3) & ~3;
+    uint32_t *vis = lds;
+    uint32_t *stk = vis + VWp;                   // v | depth << 16
+    uint32_t *ps = stk + V;                      // parent | row slot << 16
+    uint16_t *dep = reinterpret_cast<uint16_t *>(ps + V);
+    uint32_t *xch = ps + V + ((V + 1) >> 1);     // flags[2][NW], count[2]
+    const int lane = lane_id();
+    const int w = threadIdx.x >> 6;
+
+    for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
+        const int s = uniform(src[si]);
+        int32_t *prow = out_parent + (size_t)si * V;
+        int32_t *trow = out_port + (size_t)si * V;
+        int32_t *hrow = HOPS ? out_hops + (size_t)si * V : nullptr;
+        if (s < 0 || s >= V) {
+            for (int v = threadIdx.x; v < V; v += blockDim.x) {
+                prow[v] = -1;
+                trow[v] = -1;
+                if (HOPS) hrow[v] = -1;
+            }
+            continue;
+        }
+        for (int i = threadIdx.x; i < VW; i += blockDim.x) vis[i] = 0u;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            vis[s >> 5] |= 1u << (s & 31);
+            vis[V >> 5] |= 1u << (V & 31);
+            ps[s] = (uint32_t)s;
+            dep[s] = 0;
+            stk[0] = (uint32_t)s;
+        }
+        __syncthreads();
+
+        int sp = 1, par = 0;
+        while (sp > 0) {
+            const int kk = sp < K ? sp : K;
+            const int slot = w * KW + lane;
+            const int at = sp - 1 - slot;
+            uint32_t mine = stk[at < 0 ? 0 : at];
+            mine = slot < kk ? mine : (uint32_t)V;          // past the stack: sentinel row
+            uint32_t ent[KW];
+            int x[KW];
+#pragma unroll
+            for (int j = 0; j < KW; ++j) ent[j] = (uint32_t)read_lane((int)mine, j);
+#pragma unroll
+            for (int j = 0; j < KW; ++j) {
+                const uint16_t *row = adj + (size_t)(ent[j] & 0xFFFFu) * 64;
+                x[j] = row[lane];
+            }
+            uint32_t wd[KW];
+#pragma unroll
+            for (int j = 0; j < KW; ++j) wd[j] = vis[x[j] >> 5];
+            uint64_t m[KW];
+            uint32_t fl = 0;
+#pragma unroll
+            for (int j = 0; j < KW; ++j) {
+                m[j] = __ballot(((wd[j] >> (x[j] & 31)) & 1u) == 0u);
+                fl |= (m[j] != 0 ? 1u : 0u) << j;
+            }
+            if (lane == 0) xch[par * NW + w] = fl;
+            __syncthreads();
+            const uint32_t fw = xch[par * NW + (lane < NW ? lane : 0)];
+            uint64_t gm = 0;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) gm |= (uint64_t)(uint32_t)read_lane((int)fw, q) << (q * KW);
+            if (gm == 0) {                               // K leaf pops
+                sp -= kk;
+                par ^= 1;
+                continue;
+            }
+            const int istar = __ffsll((unsigned long long)gm) - 1;
+            sp -= istar + 1;
+            if (w == istar / KW) {
+                const int js = istar % KW;
+                uint64_t mm = 0;
+                int xv = 0;
+                uint32_t eu = 0;
+#pragma unroll
+                for (int j = 0; j < KW; ++j)
+                    if (j == js) {
+                        mm = m[j];
+                        xv = x[j];
+                        eu = ent[j];
+                    }
+                const int u = (int)(eu & 0xFFFFu);
+                const uint32_t dn = (eu >> 16) + 1u;
+                if ((mm >> lane) & 1ull) {
+                    atomicOr(&vis[xv >> 5], 1u << (xv & 31));
+                    ps[xv] = (uint32_t)u | ((uint32_t)lane << 16);
+                    if (HOPS) dep[xv] = (uint16_t)dn;
+                    stk[sp + lanes_below(mm)] = (uint32_t)xv | (dn << 16);
+                }
+                if (lane == 0) xch[2 * NW + par] = (uint32_t)__popcll(mm);
+            }
+            __syncthreads();
+            sp += (int)xch[2 * NW + par];
+            par ^= 1;
+        }
+        __syncthreads();
+
+        for (int v = threadIdx.x; v < V; v += blockDim.x) {
+            int p = -1, pt = -1, h = -1;
+            if ((vis[v >> 5] >> (v & 31)) & 1u) {
+                const uint32_t xx = ps[v];
+                p = (int)(xx & 0xFFFFu);
+                if (v == s) {
+                    h = 0;
+                } else {
+                    pt = port[row_ptr[p] + (int)(xx >> 16)];
+                    h = HOPS ? (int)dep[v] : 0;
+                }
+            }
+            prow[v] = p;
+            trow[v] = pt;
+            if (HOPS) hrow[v] = h;
+        }
+        __syncthreads();
+    }
+}
+
 template <typename Kern>
 void allow_full_lds(Kern kernel)
 {
@@ -578,6 +738,7 @@ struct DfsArgs {
     int nsrc;
     int32_t *parent, *port_out, *hops;
     uint2 *spill;
+    const int32_t *port_csr;
 };
 
 template <bool ELL, bool HOPS, int K>
@@ -623,6 +784,46 @@ void launch_wide(bool small, int grid, size_t lds, hipStream_t st, const DfsArgs
 
 }  // namespace
 
+static size_t dfs_lds_bytes_coop(int V)
+{
+    const size_t VWp = (size_t)((((V + 1 + 31) >> 5) + 3) & ~3);
+    return align16(4 * VWp + 8 * (size_t)V + 4 * (size_t)((V + 1) >> 1) + 4 * 32);
+}
+
+namespace {
+
+template <bool HOPS, int KW>
+void launch_coop_kw(int grid, size_t lds, hipStream_t st, int V, const uint16_t *adj,
+                    const DfsArgs &a)
+{
+    auto k = dfs_coop_kernel<4, KW, HOPS>;
+    allow_full_lds(k);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(4 * 64), lds, st, V, adj, a.row_ptr,
+                       a.port_csr, a.src, a.nsrc, a.parent, a.port_out,
+                       a.hops);
+}
+
+template <bool HOPS>
+void launch_coop(int kw, int grid, size_t lds, hipStream_t st, int V, const uint16_t *adj,
+                 const DfsArgs &a)
+{
+    if (kw >= 8) launch_coop_kw<HOPS, 8>(grid, lds, st, V, adj, a);
+    else if (kw >= 4) launch_coop_kw<HOPS, 4>(grid, lds, st, V, adj, a);
+    else launch_coop_kw<HOPS, 2>(grid, lds, st, V, adj, a);
+}
+
+}  // namespace
+
+// slots per wave of the cooperative kernel (4 waves): SDNROUTE_DFS_COOP_KW
+static int dfs_coop_kw()
+{
+    if (const char *f = getenv("SDNROUTE_DFS_COOP_KW")) {
+        const int k = atoi(f);
+        if (k == 2 || k == 4 || k == 8) return k;
+    }
+    return 4;
+}
+
 // pops checked per batch: wide rows make each leaf pop expensive, so batch
 // deeper; SDNROUTE_DFS_BATCH=1|4|8|16 overrides (tuning / tests)
 static int dfs_batch_depth(const sdnr_ctx *ctx)
@@ -650,7 +851,9 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
     // debug/test knob: SDNROUTE_DFS_STRATEGY=lds|global forces a strategy
     if (const char *f = getenv("SDNROUTE_DFS_STRATEGY")) {
         if (!strcmp(f, "global")) small = false;
-        else if (!strcmp(f, "lds") && V < 65536 && small_b <= SDNR_MAX_LDS_PER_BLOCK) small = true;
+        else if ((!strcmp(f, "lds") || !strcmp(f, "coop")) && V < 65536 &&
+                 small_b <= SDNR_MAX_LDS_PER_BLOCK)
+            small = true;
     }
     size_t lds = small ? small_b : dfs_lds_bytes_global(V);
     if (lds > SDNR_MAX_LDS_PER_BLOCK)
@@ -668,9 +871,24 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         spill = static_cast<uint2 *>(ctx->scratch);
     }
     DfsArgs a{V, ctx->W, ctx->row_ptr, ell ? ctx->ell_col : ctx->col,
-              ell ? ctx->ell_port : ctx->port, d_src, nsrc, d_parent, d_port, d_hops, spill};
+              ell ? ctx->ell_port : ctx->port, d_src, nsrc, d_parent, d_port, d_hops, spill,
+              ctx->port};
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
-    if (narrow) {
+    const char *force = getenv("SDNROUTE_DFS_STRATEGY");
+    const bool coop_ok = ctx->adj16 != nullptr && V < 65535 &&
+                         dfs_lds_bytes_coop(V) <= SDNR_MAX_LDS_PER_BLOCK;
+    const bool coop = coop_ok && (force ? !strcmp(force, "coop") : small);
+    if (coop) {
+        const size_t cl = dfs_lds_bytes_coop(V);
+        size_t cpc = SDNR_LDS_PER_CU / cl;
+        if (cpc > 8) cpc = 8;
+        if (cpc < 1) cpc = 1;
+        int cgrid = (int)((size_t)ctx->num_cus * cpc);
+        if (cgrid > nsrc) cgrid = nsrc;
+        const int kw = dfs_coop_kw();
+        if (hops) launch_coop<true>(kw, cgrid, cl, ctx->stream, V, ctx->adj16, a);
+        else launch_coop<false>(kw, cgrid, cl, ctx->stream, V, ctx->adj16, a);
+    } else if (narrow) {
         const int K = dfs_batch_depth(ctx);
         if (ell && hops) launch_batch_k<true, true>(K, small, grid, lds, ctx->stream, a);
         else if (ell) launch_batch_k<true, false>(K, small, grid, lds, ctx->stream, a);
