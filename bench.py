@@ -39,6 +39,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from sdnmpi_amd import _native  # noqa: E402
+from sdnmpi_amd import distributed as D  # noqa: E402
 from sdnmpi_amd import topologies as T  # noqa: E402
 
 METRIC = "all-pairs routes/sec + % HBM roofline, k=48 fat-tree, 1/2/4/8 MI355X"
@@ -140,17 +141,15 @@ def main():
     srcs = srcs.astype(np.int32)
     H = fabric.n_hosts
     S = len(srcs)
-    per = (S + world - 1) // world
-    lo, hi = min(S, rank * per), min(S, (rank + 1) * per)
-    my = np.full(per, -1, np.int32)          # pad: out-of-range id -> empty row
-    my[: hi - lo] = srcs[lo:hi]
+    lo, hi, per = D.shard_bounds(S, world, rank)
+    my = D.padded_shard(srcs, world, rank)   # pad: id -1 -> empty row
 
     ctx = _native.Context(local)
     ctx.upload(csr)
     stream = torch.cuda.Stream(dev)       # the kernels' stream (events go here)
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
-    t_src = torch.from_numpy(my).to(dev)
+    t_src = my.to(dev)
     if args.mode == "dfs":
         a = torch.empty((per, V), dtype=torch.int32, device=dev)     # parent
         b = torch.empty((per, V), dtype=torch.int32, device=dev)     # port
@@ -159,10 +158,6 @@ def main():
         a = torch.empty((per, V), dtype=torch.int16, device=dev)     # dist (u16)
         b = torch.empty((per, V), dtype=torch.int32, device=dev)     # nh
         c = torch.empty((per, V), dtype=torch.int32, device=dev)     # nh_port
-    if world > 1:
-        ga = torch.empty((world * per, V), dtype=a.dtype, device=dev)
-        gb = torch.empty((world * per, V), dtype=b.dtype, device=dev)
-        gc = torch.empty((world * per, V), dtype=c.dtype, device=dev) if c is not None else None
 
     def step(ev=None):
         if ev is not None:
@@ -174,11 +169,10 @@ def main():
                                        c.data_ptr())
         if ev is not None:
             ev[1].record(stream)
-        if world > 1:
-            dist.all_gather_into_tensor(ga, a)
-            dist.all_gather_into_tensor(gb, b)
-            if c is not None:
-                dist.all_gather_into_tensor(gc, c)
+        if world > 1:                       # assemble [sources][V] on every rank
+            for t in (a, b, c):
+                if t is not None:
+                    D.all_gather_rows(t)
 
     for _ in range(args.warmup):
         step()

@@ -58,8 +58,13 @@ static void free_graph(sdnr_ctx *c)
         if (*b) (void)hipFree(*b);
         *b = nullptr;
     }
+    if (c->radj16 && c->radj_owned) (void)hipFree(c->radj16);
     if (c->adj16) (void)hipFree(c->adj16);
+    if (c->deg2) (void)hipFree(c->deg2);
     c->adj16 = nullptr;
+    c->radj16 = nullptr;
+    c->deg2 = nullptr;
+    c->radj_owned = false;
     c->V = -1;
     c->E = 0;
     c->W = 0;
@@ -216,17 +221,53 @@ int sdnr_graph_upload(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_pt
         }
         SDNR_HIP(hipStreamSynchronize(ctx->stream));   // before ec/ep go away
     }
-    // u16 rows of stride 64 (one 128-byte line) for the cooperative DFS:
-    // padding and the extra row V hold the sentinel vertex V
+    // u16 rows of stride 64 (one 128-byte line) for the cooperative DFS
+    // kernels: padding and the extra row V hold the sentinel vertex V; the
+    // in-neighbour rows (same layout) and packed out-degrees feed the
+    // counted-pop kernel
     if (V < 65535 && maxdeg <= SDNR_WAVE) {
-        std::vector<uint16_t> a16(((size_t)V + 1) * SDNR_WAVE, (uint16_t)V);
-        for (int32_t u = 0; u < V; ++u)
-            for (int32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e)
+        const size_t rows = ((size_t)V + 1) * SDNR_WAVE;
+        std::vector<uint16_t> a16(rows, (uint16_t)V), r16(rows, (uint16_t)V);
+        std::vector<int32_t> indeg((size_t)V + 1, 0);
+        std::vector<uint32_t> d2(((size_t)V + 2) / 2 + 4, 0u);
+        for (int32_t u = 0; u < V; ++u) {
+            const int32_t d = row_ptr[u + 1] - row_ptr[u];
+            d2[(size_t)u >> 1] |= (uint32_t)d << ((u & 1) * 16);
+            for (int32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) {
                 a16[(size_t)u * SDNR_WAVE + (e - row_ptr[u])] = (uint16_t)col[e];
-        const size_t bytes = a16.size() * sizeof(uint16_t);
-        hipError_t he = hipMalloc(reinterpret_cast<void **>(&ctx->adj16), bytes);
+                indeg[col[e]]++;
+            }
+        }
+        int32_t maxin = 0;
+        for (int32_t v = 0; v < V; ++v) maxin = indeg[v] > maxin ? indeg[v] : maxin;
+        bool sym = true;
+        if (maxin <= SDNR_WAVE) {
+            std::vector<int32_t> fill((size_t)V, 0);
+            for (int32_t u = 0; u < V; ++u)       // ascending u: rows come out sorted
+                for (int32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) {
+                    const int32_t v = col[e];
+                    r16[(size_t)v * SDNR_WAVE + fill[v]++] = (uint16_t)u;
+                }
+            sym = a16 == r16;
+        }
+        hipError_t he = hipMalloc(reinterpret_cast<void **>(&ctx->adj16), rows * 2);
         if (he == hipSuccess)
-            he = hipMemcpyAsync(ctx->adj16, a16.data(), bytes, hipMemcpyHostToDevice, ctx->stream);
+            he = hipMemcpyAsync(ctx->adj16, a16.data(), rows * 2, hipMemcpyHostToDevice, ctx->stream);
+        if (he == hipSuccess && maxin <= SDNR_WAVE) {
+            he = hipMalloc(reinterpret_cast<void **>(&ctx->deg2), d2.size() * 4);
+            if (he == hipSuccess)
+                he = hipMemcpyAsync(ctx->deg2, d2.data(), d2.size() * 4, hipMemcpyHostToDevice,
+                                    ctx->stream);
+            if (he == hipSuccess && sym) {
+                ctx->radj16 = ctx->adj16;
+            } else if (he == hipSuccess) {
+                he = hipMalloc(reinterpret_cast<void **>(&ctx->radj16), rows * 2);
+                ctx->radj_owned = he == hipSuccess;
+                if (he == hipSuccess)
+                    he = hipMemcpyAsync(ctx->radj16, r16.data(), rows * 2, hipMemcpyHostToDevice,
+                                        ctx->stream);
+            }
+        }
         if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
         if (he != hipSuccess) {
             free_graph(ctx);

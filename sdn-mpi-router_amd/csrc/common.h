@@ -46,6 +46,9 @@ struct sdnr_ctx {
     int32_t *row_ptr = nullptr, *col = nullptr, *port = nullptr;
     int32_t *ell_col = nullptr, *ell_port = nullptr;
     uint16_t *adj16 = nullptr;          // (V+1) rows x 64 u16, sentinel V (V < 65535)
+    uint16_t *radj16 = nullptr;         // in-neighbour rows, same layout (== adj16 if symmetric)
+    uint32_t *deg2 = nullptr;           // out-degrees of 0..V as u16 pairs
+    bool radj_owned = false;
 
     // grow-only device scratch / staging
     void *scratch = nullptr;

@@ -707,6 +707,151 @@ __global__ __launch_bounds__(NW * 64) void dfs_coop_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Counted pops (small graphs with in/out-degree <= 64): the k=48 headline.
+//
+// cnt[u] = number of out-neighbours of u not yet visited.  A pop is a leaf
+// pop exactly when cnt[u] == 0, so runs of leaf pops are skipped 64 stack
+// entries at a time: one LDS read of the stack slots, one gather of their
+// counts, one ballot -- no adjacency row is touched.  The price is moved to
+// push time, where it is parallel: a vertex v that becomes visited
+// decrements cnt[x] for every in-neighbour x (its reverse row, loaded with
+// the other children's rows in flight together, then ds_sub_u32 on packed
+// u16 pairs -- a count never drops below zero, so no borrow crosses halves).
+// Only the non-leaf pops (~4% on the k=48 fat-tree) load a forward row and
+// gather visited bits.  A workgroup of NW waves owns one source: every wave
+// runs the skip and the row check redundantly (same LDS state, same result,
+// no exchange), wave 0 writes marks/stack/tree, the children's decrements
+// are split round-robin over the waves; barrier A separates the visited
+// gathers from the marks, barrier B publishes the push.
+// ---------------------------------------------------------------------------
+template <int NW, bool HOPS>
+__global__ __launch_bounds__(NW * 64) void dfs_count_kernel(
+    int V, const uint16_t *__restrict__ adj, const uint16_t *__restrict__ radj,
+    const uint32_t *__restrict__ deg2, const int32_t *__restrict__ row_ptr,
+    const int32_t *__restrict__ port, const int32_t *__restrict__ src, int nsrc,
+    int32_t *__restrict__ out_parent, int32_t *__restrict__ out_port,
+    int32_t *__restrict__ out_hops)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int VW = (V + 1 + 31) >> 5;            // + sentinel bit V
+    const int VWp = (VW + 3) & ~3;
+    const int CW = (V + 2) >> 1;                 // u16 counts of 0..V, in pairs
+    const int CWp = (CW + 3) & ~3;
+    const int SWp = (((V + 1) >> 1) + 3) & ~3;   // u16 stack / depth words
+    uint32_t *vis = lds;
+    uint32_t *cnt = vis + VWp;
+    uint16_t *stk = reinterpret_cast<uint16_t *>(cnt + CWp);
+    uint32_t *ps = cnt + CWp + SWp;              // parent | row slot << 16
+    uint16_t *dep = reinterpret_cast<uint16_t *>(ps + V);
+    const int lane = lane_id();
+    const int w = threadIdx.x >> 6;
+
+    for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
+        const int s = uniform(src[si]);
+        int32_t *prow = out_parent + (size_t)si * V;
+        int32_t *trow = out_port + (size_t)si * V;
+        int32_t *hrow = HOPS ? out_hops + (size_t)si * V : nullptr;
+        if (s < 0 || s >= V) {
+            for (int v = threadIdx.x; v < V; v += blockDim.x) {
+                prow[v] = -1;
+                trow[v] = -1;
+                if (HOPS) hrow[v] = -1;
+            }
+            continue;
+        }
+        for (int i = threadIdx.x; i < VW; i += blockDim.x) vis[i] = 0u;
+        for (int i = threadIdx.x; i < CW; i += blockDim.x) cnt[i] = deg2[i];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            vis[s >> 5] |= 1u << (s & 31);
+            vis[V >> 5] |= 1u << (V & 31);
+            ps[s] = (uint32_t)s;
+            if (HOPS) dep[s] = 0;
+            stk[0] = (uint16_t)s;
+        }
+        if (w == 0) {                            // s is visited: its in-neighbours lose one
+            const int r = radj[(size_t)s * 64 + lane];
+            if (r != V) atomicSub(&cnt[r >> 1], (r & 1) ? 0x10000u : 1u);
+        }
+        __syncthreads();
+
+        int sp = 1;
+        for (;;) {
+            // ---- skip leaf pops, 64 stack slots per step
+            uint64_t m = 0;
+            int e = V;
+            while (sp > 0) {
+                const int kk = sp < 64 ? sp : 64;
+                const int at = sp - 1 - lane;
+                e = stk[at < 0 ? 0 : at];
+                e = lane < kk ? e : V;
+                const uint32_t c = (cnt[e >> 1] >> ((e & 1) << 4)) & 0xFFFFu;
+                m = __ballot(c != 0u);
+                if (m) break;
+                sp -= kk;
+            }
+            if (!m) break;
+            const int first = __ffsll((unsigned long long)m) - 1;
+            const int u = read_lane(e, first);
+            sp -= first + 1;
+            // ---- the non-leaf pop: forward row, visited gather
+            const int x = adj[(size_t)u * 64 + lane];
+            const uint32_t wv = vis[x >> 5];
+            const bool fresh = ((wv >> (x & 31)) & 1u) == 0u;
+            const uint64_t mm = __ballot(fresh);
+            const int rank = lanes_below(mm);
+            int du = 0;
+            if (HOPS) du = uniform((int)dep[u]);
+            __syncthreads();                     // A: gathers before marks
+            if (w == 0 && fresh) {
+                atomicOr(&vis[x >> 5], 1u << (x & 31));
+                ps[x] = (uint32_t)u | ((uint32_t)lane << 16);
+                if (HOPS) dep[x] = (uint16_t)(du + 1);
+                stk[sp + rank] = (uint16_t)x;
+            }
+            // ---- children decrement their in-neighbours' counts
+            uint64_t mine = __ballot(fresh && (rank % NW) == w);
+            while (mine) {
+                int r[4];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    int v = V;
+                    if (mine) {
+                        v = read_lane(x, __ffsll((unsigned long long)mine) - 1);
+                        mine &= mine - 1;
+                    }
+                    r[g] = radj[(size_t)v * 64 + lane];
+                }
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    if (r[g] != V) atomicSub(&cnt[r[g] >> 1], (r[g] & 1) ? 0x10000u : 1u);
+            }
+            sp += __popcll(mm);
+            __syncthreads();                     // B: publish the push
+        }
+        __syncthreads();
+
+        for (int v = threadIdx.x; v < V; v += blockDim.x) {
+            int p = -1, pt = -1, h = -1;
+            if ((vis[v >> 5] >> (v & 31)) & 1u) {
+                const uint32_t xx = ps[v];
+                p = (int)(xx & 0xFFFFu);
+                if (v == s) {
+                    h = 0;
+                } else {
+                    pt = port[row_ptr[p] + (int)(xx >> 16)];
+                    h = HOPS ? (int)dep[v] : 0;
+                }
+            }
+            prow[v] = p;
+            trow[v] = pt;
+            if (HOPS) hrow[v] = h;
+        }
+        __syncthreads();
+    }
+}
+
 template <typename Kern>
 void allow_full_lds(Kern kernel)
 {
@@ -784,6 +929,14 @@ void launch_wide(bool small, int grid, size_t lds, hipStream_t st, const DfsArgs
 
 }  // namespace
 
+static size_t dfs_lds_bytes_count(int V, bool hops)
+{
+    const size_t VWp = (size_t)((((V + 1 + 31) >> 5) + 3) & ~3);
+    const size_t CWp = (size_t)((((V + 2) >> 1) + 3) & ~3);
+    const size_t SWp = (size_t)((((V + 1) >> 1) + 3) & ~3);
+    return align16(4 * (VWp + CWp + SWp) + 4 * (size_t)V + (hops ? 2 * (size_t)V : 0));
+}
+
 static size_t dfs_lds_bytes_coop(int V)
 {
     const size_t VWp = (size_t)((((V + 1 + 31) >> 5) + 3) & ~3);
@@ -851,7 +1004,7 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
     // debug/test knob: SDNROUTE_DFS_STRATEGY=lds|global forces a strategy
     if (const char *f = getenv("SDNROUTE_DFS_STRATEGY")) {
         if (!strcmp(f, "global")) small = false;
-        else if ((!strcmp(f, "lds") || !strcmp(f, "coop")) && V < 65536 &&
+        else if ((!strcmp(f, "lds") || !strcmp(f, "coop") || !strcmp(f, "count")) && V < 65536 &&
                  small_b <= SDNR_MAX_LDS_PER_BLOCK)
             small = true;
     }
@@ -875,10 +1028,31 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
               ctx->port};
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
     const char *force = getenv("SDNROUTE_DFS_STRATEGY");
+    const bool count_ok = ctx->adj16 != nullptr && ctx->radj16 != nullptr && V < 65535 &&
+                          dfs_lds_bytes_count(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;
+    const bool count = count_ok && (force ? !strcmp(force, "count") : small);
     const bool coop_ok = ctx->adj16 != nullptr && V < 65535 &&
                          dfs_lds_bytes_coop(V) <= SDNR_MAX_LDS_PER_BLOCK;
-    const bool coop = coop_ok && (force ? !strcmp(force, "coop") : small);
-    if (coop) {
+    const bool coop = !count && coop_ok && (force ? !strcmp(force, "coop") : small);
+    if (count) {
+        const size_t cl = dfs_lds_bytes_count(V, hops);
+        size_t cpc = SDNR_LDS_PER_CU / cl;
+        if (cpc > 8) cpc = 8;
+        if (cpc < 1) cpc = 1;
+        int cgrid = (int)((size_t)ctx->num_cus * cpc);
+        if (cgrid > nsrc) cgrid = nsrc;
+#define SDNR_COUNT(H_)                                                                       \
+    do {                                                                                     \
+        auto k = dfs_count_kernel<4, H_>;                                                    \
+        allow_full_lds(k);                                                                   \
+        hipLaunchKernelGGL(k, dim3(cgrid), dim3(256), cl, ctx->stream, V, ctx->adj16,        \
+                           ctx->radj16, ctx->deg2, ctx->row_ptr, ctx->port, d_src, nsrc,     \
+                           d_parent, d_port, d_hops);                                        \
+    } while (0)
+        if (hops) SDNR_COUNT(true);
+        else SDNR_COUNT(false);
+#undef SDNR_COUNT
+    } else if (coop) {
         const size_t cl = dfs_lds_bytes_coop(V);
         size_t cpc = SDNR_LDS_PER_CU / cl;
         if (cpc > 8) cpc = 8;

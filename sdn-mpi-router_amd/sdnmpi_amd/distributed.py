@@ -1,0 +1,57 @@
+"""Source-sharded route tables over the GPUs of one node.
+
+Every source tree (DFS mode) / destination table (shortest mode) is
+independent, so the table rows shard with no communication in the compute:
+rank r builds rows [r*per, (r+1)*per) of the padded source list on its own
+GPU, and ONE all-gather (RCCL over xGMI with the "nccl" backend, gloo on CPU
+for tests) assembles the full [sources][V] tables on every rank -- the
+exchange step the controller needs to answer any (src, dst) from any rank.
+
+The padded tail of the last shard uses source id -1, which the kernels turn
+into an all-(-1) row; ``unpad`` drops it after the gather.
+"""
+
+import torch
+import torch.distributed as dist
+
+__all__ = ["shard_bounds", "padded_shard", "all_gather_rows", "unpad"]
+
+
+def shard_bounds(n, world, rank):
+    """(lo, hi, per): rank's rows [lo, hi) of n, every rank padded to per."""
+    per = (n + world - 1) // world if world > 0 else n
+    lo = min(n, rank * per)
+    hi = min(n, lo + per)
+    return lo, hi, per
+
+
+def padded_shard(ids, world, rank):
+    """This rank's source ids, padded with -1 to the common shard length."""
+    lo, hi, per = shard_bounds(len(ids), world, rank)
+    out = torch.full((per,), -1, dtype=torch.int32)
+    if hi > lo:
+        out[: hi - lo] = torch.as_tensor(ids[lo:hi], dtype=torch.int32)
+    return out
+
+
+def all_gather_rows(local, group=None):
+    """[per, V] on every rank -> [world*per, V] on every rank, rank order.
+
+    One collective per table; on the nccl backend this is RCCL's all-gather
+    over xGMI, writing straight into the assembled tensor.
+    """
+    world = dist.get_world_size(group)
+    if world == 1:
+        return local
+    out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]),
+                      dtype=local.dtype, device=local.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, local.contiguous(), group=group)
+    else:   # gloo has no all_gather_into_tensor for every dtype
+        parts = list(out.chunk(world, 0))
+        dist.all_gather(parts, local.contiguous(), group=group)
+    return out
+
+
+def unpad(table, n):
+    return table[:n]

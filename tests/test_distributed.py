@@ -1,0 +1,75 @@
+"""Multi-rank table assembly on CPU (gloo, world_size 2 and 3): each rank
+builds its shard of the per-source tables (oracle stands in for the GPU
+kernel here), one all-gather assembles them, and the result must equal the
+single-process table bit for bit -- including the -1 padding of the last
+shard and uneven source counts."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, fabric_name, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "sdn-mpi-router_amd")]
+    from oracle import oracle as O
+    from sdnmpi_amd import distributed as D
+    from sdnmpi_amd import topologies as T
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fabric = T.by_name(fabric_name)
+        csr = fabric.csr()
+        srcs = np.unique(fabric.host_table()[0]).astype(np.int32)
+        mine = D.padded_shard(srcs, world, rank).numpy()
+        # stand-in for the kernel: rows of -1 for padded (-1) sources
+        ok = mine >= 0
+        parent = np.full((len(mine), csr.V), -1, np.int32)
+        port = np.full((len(mine), csr.V), -1, np.int32)
+        if ok.any():
+            p, t, _ = O.dfs_tables(csr, mine[ok], with_hops=False, nthreads=1)
+            parent[ok], port[ok] = p, t
+        gp = D.unpad(D.all_gather_rows(torch.from_numpy(parent)), len(srcs))
+        gt = D.unpad(D.all_gather_rows(torch.from_numpy(port)), len(srcs))
+        if rank == 0:
+            po, to, _ = O.dfs_tables(csr, srcs, with_hops=False, nthreads=1)
+            q.put(bool(np.array_equal(gp.numpy(), po) and np.array_equal(gt.numpy(), to)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fabric", [(2, "fat_tree:8"), (3, "dragonfly:4,2,2")])
+def test_sharded_tables_assemble_exactly(world, fabric):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fabric, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=10) is True
+
+
+def test_shard_bounds_cover_everything():
+    from sdnmpi_amd.distributed import shard_bounds
+    for n in (0, 1, 7, 1152, 1153):
+        for world in (1, 2, 3, 8):
+            rows = []
+            for r in range(world):
+                lo, hi, per = shard_bounds(n, world, r)
+                assert hi - lo <= per
+                rows += list(range(lo, hi))
+            assert rows == list(range(n))

@@ -57,7 +57,7 @@ def _check_pairs(g, fabric, p, t, srcs):
         assert got == g.fdb(i), (g.name, i)
 
 
-@pytest.mark.parametrize("strategy", ["auto", "coop", "lds", "global"])
+@pytest.mark.parametrize("strategy", ["auto", "count", "coop", "lds", "global"])
 @pytest.mark.parametrize("ell", [True, False])
 @pytest.mark.parametrize("name", G.SMALL)
 def test_dfs_small_all_sources(ctx, monkeypatch, name, strategy, ell):

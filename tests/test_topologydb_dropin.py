@@ -1,0 +1,212 @@
+"""The drop-in TopologyDB, exercised the way the reference uses it.
+
+* ``TestReferenceSuite`` re-states the reference's own unit tests
+  (reference ``tests/test_topologydb.py:13-109``: 4-switch square fixture,
+  dicts assigned directly, ``del`` of a links entry) against our class.
+* scenario replays (tests/golden/scenarios.json, produced by the reference):
+  mutations through the methods AND directly on the dicts, deleted switches
+  whose links stay, parallel links, switch-local MACs (OFPP_LOCAL), unknown
+  and malformed MACs -- every query's result must equal the reference's.
+* every host pair of the small golden fabrics, both route modes.
+
+GPU tests: routes come from the HIP tables.  The CPU-only tests at the end
+check the host-side logic (dict tracking / invalidation) with a fake engine.
+"""
+import numpy as np
+import pytest
+
+import golden_util as G
+from sdnmpi_amd.objects import Host, Link, Port, Switch
+from sdnmpi_amd.util.topology_db import OFPP_LOCAL, TopologyDB
+
+MAC1 = "02:00:00:00:00:01"
+MAC2 = "02:00:00:00:00:02"
+MAC3 = "02:00:00:00:00:03"
+MAC4 = "02:00:00:00:00:04"
+
+
+def square_db():
+    """Reference fixture: tests/test_topologydb.py:14-61."""
+    db = TopologyDB()
+    p = {(d, n): Port(d, n) for d in (1, 2, 3, 4) for n in (1, 2, 3)}
+    db.links = {
+        1: {2: Link(p[1, 2], p[2, 2]), 3: Link(p[1, 3], p[3, 3])},
+        2: {1: Link(p[2, 2], p[1, 2]), 4: Link(p[2, 3], p[4, 2])},
+        3: {1: Link(p[3, 3], p[1, 3]), 4: Link(p[3, 2], p[4, 3])},
+        4: {2: Link(p[4, 2], p[2, 3]), 3: Link(p[4, 3], p[3, 2])},
+    }
+    db.hosts = {MAC1: Host(MAC1, p[1, 1]), MAC2: Host(MAC2, p[2, 1]),
+                MAC3: Host(MAC3, p[3, 1]), MAC4: Host(MAC4, p[4, 1])}
+    db.switches = {d: Switch(d) for d in (1, 2, 3, 4)}
+    return db
+
+
+@pytest.mark.gpu
+class TestReferenceSuite(object):
+    def test_find_route_same_switch(self):
+        db = square_db()
+        for mac, d in ((MAC1, 1), (MAC2, 2), (MAC3, 3), (MAC4, 4)):
+            assert db.find_route(mac, mac) == [(d, 1)]
+
+    def test_find_route_unreachable(self):
+        db = square_db()
+        del db.links[1]
+        assert db.find_route(MAC1, MAC2) == []
+        assert db.find_route(MAC1, MAC3) == []
+        assert db.find_route(MAC1, MAC4) == []
+
+    def test_find_route_between_switches(self):
+        db = square_db()
+        assert db.find_route(MAC1, MAC2) == [(1, 2), (2, 1)]
+        assert db.find_route(MAC1, MAC3) == [(1, 3), (3, 1)]
+        assert db.find_route(MAC2, MAC4) == [(2, 3), (4, 1)]
+        assert db.find_route(MAC3, MAC4) == [(3, 2), (4, 1)]
+
+    def test_find_multiple_routes(self):
+        db = square_db()
+        routes = db.find_route(MAC1, MAC4, True)
+        assert sorted(routes) == sorted([[(1, 2), (2, 3), (4, 1)], [(1, 3), (3, 2), (4, 1)]])
+        assert sorted(db.find_route(MAC3, MAC4, True)) == [[(3, 2), (4, 1)]]
+
+    def test_find_multiple_routes_unreachable(self):
+        db = square_db()
+        del db.links[1]
+        for mac in (MAC2, MAC3, MAC4):
+            assert db.find_route(MAC1, mac, True) == []
+
+    def test_dfs_is_not_shortest_and_local_ports(self):
+        """SURVEY.md section 4 all-pairs fixture: 1->4 goes via 3 (LIFO takes
+        the largest branch), switch-local destinations end in OFPP_LOCAL."""
+        db = square_db()
+        assert db.find_route(MAC1, MAC4) == [(1, 3), (3, 2), (4, 1)]
+        assert db.find_route(MAC4, MAC1) == [(4, 3), (3, 3), (1, 1)]
+        assert db.find_route(MAC1, "00:00:00:00:00:04") == [(1, 3), (3, 2), (4, OFPP_LOCAL)]
+        assert db.find_route("00:00:00:00:00:04", MAC1) == [(4, 3), (3, 3), (1, 1)]
+        assert db.find_route(MAC1, "02:00:00:00:00:99") == []
+
+    def test_return_types_are_python_ints(self):
+        db = square_db()
+        for hop in db.find_route(MAC1, MAC4) + db.find_route(MAC1, MAC4, True)[0]:
+            assert type(hop) is tuple and all(type(x) is int for x in hop)
+
+
+@pytest.mark.gpu
+def test_scenarios_match_reference():
+    db = TopologyDB()
+    for sc in G.scenarios():
+        for op in sc["ops"]:
+            G.apply_op(db, op)
+        for a, b, multiple, want in sc.get("queries", []):
+            assert db.find_route(a, b, multiple) == G.as_tuples(want), (sc["name"], a, b, multiple)
+        for a, b, exc in sc.get("raises", []):
+            with pytest.raises(Exception) as ei:
+                db.find_route(a, b)
+            assert type(ei.value).__name__ == exc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", G.SMALL)
+def test_all_host_pairs_match_reference(name):
+    g = G.Golden(name)
+    fabric = g.fabric()
+    db = fabric.populate(TopologyDB())
+    macs = fabric.host_macs()
+    pairs = [(macs[a], macs[b]) for a, b in zip(g.pair_src, g.pair_dst)]
+    got = db.find_routes(pairs)
+    for i, r in enumerate(got):
+        assert r == g.fdb(i), (name, i)
+    if g.has_multi():
+        for i, (a, b) in enumerate(pairs):
+            assert db.find_route(a, b, True) == g.multi(i), (name, i)
+
+
+@pytest.mark.gpu
+def test_route_tables_batched_form():
+    from oracle import oracle as O
+    fabric = G.Golden("fat_tree_k8").fabric()
+    db = fabric.populate(TopologyDB())
+    t = db.route_tables("dfs")
+    csr = fabric.csr()
+    po, to, ho = O.dfs_tables(csr, t["sources"])
+    np.testing.assert_array_equal(t["parent"], po)
+    np.testing.assert_array_equal(t["port"], to)
+    np.testing.assert_array_equal(t["hops"], ho)
+    s = db.route_tables("shortest")
+    do, nho, nhpo = O.dest_tables(csr, s["destinations"])
+    np.testing.assert_array_equal(s["dist"], do)
+    np.testing.assert_array_equal(s["nh"], nho)
+    np.testing.assert_array_equal(s["nh_port"], nhpo)
+
+
+# ----------------------------------------------------------------- CPU only --
+
+class _FakeEngine(object):
+    """Test double for RouteEngine: oracle tables + a call log."""
+
+    def __init__(self):
+        from oracle import oracle as O
+        self.O = O
+        self.calls = []
+
+    def dfs_tables(self, export, srcs, with_hops=True):
+        self.calls.append(("dfs", export.key, tuple(int(x) for x in srcs)))
+        return self.O.dfs_tables(export.csr, srcs)
+
+    def shortest_tables(self, export, dsts):
+        self.calls.append(("sp", export.key, tuple(int(x) for x in dsts)))
+        return self.O.dest_tables(export.csr, dsts)
+
+
+def test_dict_mutations_invalidate_tables():
+    eng = _FakeEngine()
+    db = square_db()
+    db._engine = eng
+    assert db.find_route(MAC1, MAC2) == [(1, 2), (2, 1)]
+    n = len(eng.calls)
+    assert db.find_route(MAC3, MAC4) == [(3, 2), (4, 1)]     # cached: no new call
+    assert len(eng.calls) == n
+    del db.links[1][2]                                      # nested dict mutation
+    assert db.find_route(MAC1, MAC2) == [(1, 3), (3, 2), (4, 2), (2, 1)]
+    assert len(eng.calls) == n + 1
+    db.links[1][2] = Link(Port(1, 7), Port(2, 2))            # re-add, new port
+    assert db.find_route(MAC1, MAC2) == [(1, 7), (2, 1)]
+    db.links = {}                                           # whole-dict assignment
+    assert db.find_route(MAC1, MAC2) == []
+
+
+def test_host_only_changes_keep_tables():
+    eng = _FakeEngine()
+    db = square_db()
+    db._engine = eng
+    db.find_route(MAC1, MAC4)
+    n = len(eng.calls)
+    db.add_host(Host(MAC4, Port(4, 9)))                    # same switch, new port
+    assert db.find_route(MAC1, MAC4) == [(1, 3), (3, 2), (4, 9)]
+    assert len(eng.calls) == n                             # graph unchanged
+
+
+def test_find_route_errors_before_engine():
+    db = square_db()
+    db._engine = None
+    with pytest.raises(ValueError):
+        db.find_route("zz:00:00:00:00:01", MAC2)
+    assert db.find_route("02:00:00:00:00:77", MAC2) == []   # unknown host: no engine needed
+    assert db._engine is None
+
+
+def test_to_dict_snapshot():
+    db = square_db()
+    d = db.to_dict()
+    assert len(d["links"]) == 8 and len(d["hosts"]) == 4 and len(d["switches"]) == 4
+
+
+def test_tracked_dicts_are_dicts():
+    db = square_db()
+    assert isinstance(db.links, dict) and isinstance(db.links[1], dict)
+    assert sorted(db.links[1].keys()) == [2, 3]
+    v = db._versions.key()
+    db.links.setdefault(9, {})[1] = Link(Port(9, 1), Port(1, 5))
+    assert db._versions.key() != v
+    v = db._versions.key()
+    db.links[9].pop(1)
+    assert db._versions.key() != v
