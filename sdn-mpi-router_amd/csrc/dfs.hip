@@ -777,6 +777,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_count_kernel(
         __syncthreads();
 
         int sp = 1;
+        int pu = -1, xpre = V;                   // speculatively loaded row of pu
         for (;;) {
             // ---- skip leaf pops, 64 stack slots per step
             uint64_t m = 0;
@@ -795,12 +796,15 @@ __global__ __launch_bounds__(NW * 64) void dfs_count_kernel(
             const int first = __ffsll((unsigned long long)m) - 1;
             const int u = read_lane(e, first);
             sp -= first + 1;
-            // ---- the non-leaf pop: forward row, visited gather
-            const int x = adj[(size_t)u * 64 + lane];
+            // ---- the non-leaf pop: forward row (usually prefetched: the
+            // top of the stack is the previous push's largest child), visited gather
+            const int x = (u == pu) ? xpre : (int)adj[(size_t)u * 64 + lane];
             const uint32_t wv = vis[x >> 5];
             const bool fresh = ((wv >> (x & 31)) & 1u) == 0u;
             const uint64_t mm = __ballot(fresh);
             const int rank = lanes_below(mm);
+            pu = read_lane(x, highest_lane(mm));     // cnt[u] != 0 -> mm != 0
+            xpre = adj[(size_t)pu * 64 + lane];
             int du = 0;
             if (HOPS) du = uniform((int)dep[u]);
             __syncthreads();                     // A: gathers before marks
@@ -812,10 +816,11 @@ __global__ __launch_bounds__(NW * 64) void dfs_count_kernel(
             }
             // ---- children decrement their in-neighbours' counts
             uint64_t mine = __ballot(fresh && (rank % NW) == w);
-            while (mine) {
-                int r[4];
+            while (mine) {                       // all of a wave's rows in flight together
+                constexpr int G = 64 / NW < 16 ? 64 / NW : 16;
+                int r[G];
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
+                for (int g = 0; g < G; ++g) {
                     int v = V;
                     if (mine) {
                         v = read_lane(x, __ffsll((unsigned long long)mine) - 1);
@@ -824,7 +829,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_count_kernel(
                     r[g] = radj[(size_t)v * 64 + lane];
                 }
 #pragma unroll
-                for (int g = 0; g < 4; ++g)
+                for (int g = 0; g < G; ++g)
                     if (r[g] != V) atomicSub(&cnt[r[g] >> 1], (r[g] & 1) ? 0x10000u : 1u);
             }
             sp += __popcll(mm);
@@ -847,6 +852,146 @@ __global__ __launch_bounds__(NW * 64) void dfs_count_kernel(
             prow[v] = p;
             trow[v] = pt;
             if (HOPS) hrow[v] = h;
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Lane-packed batched pops for large, low-degree graphs (torus 32^3: 6,
+// Jellyfish: 16).  A row needs only LPR >= W lanes, so one wave instruction
+// checks R = 64/LPR stack entries (lane l -> slot l/LPR, row position l%LPR)
+// and J instructions check K = R*J entries: R times fewer loads, gathers and
+// ballots per pop than one-row-per-wavefront.  Same exact semantics as
+// dfs_global_batch_kernel (first live entry from the top is processed).
+// ---------------------------------------------------------------------------
+template <int LPR, int J, bool HOPS>
+__global__ __launch_bounds__(64) void dfs_global_packed_kernel(
+    int V, int W, const int32_t *__restrict__ col, const int32_t *__restrict__ port,
+    const int32_t *__restrict__ src, int nsrc, int32_t *__restrict__ out_parent,
+    int32_t *__restrict__ out_port, int32_t *__restrict__ out_hops,
+    uint2 *__restrict__ spill_all)
+{
+    constexpr int R = 64 / LPR;
+    constexpr int K = R * J;
+    static_assert(K <= 64, "one stack slot per lane");
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int VW = (V + 31) >> 5;
+    const int VWp = (VW + 3) & ~3;
+    uint32_t *vis = lds;
+    uint2 *ring = reinterpret_cast<uint2 *>(vis + VWp);   // (v, depth)
+    uint2 *spill = spill_all + (size_t)blockIdx.x * (size_t)V;
+    const int lane = lane_id();
+    const int pos = lane % LPR;
+    const int sub = lane / LPR;
+    const uint64_t lowmask = (LPR == 64) ? ~0ull : ((1ull << LPR) - 1ull);
+
+    for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
+        const int s = uniform(src[si]);
+        int32_t *prow = out_parent + (size_t)si * V;
+        int32_t *trow = out_port + (size_t)si * V;
+        int32_t *hrow = HOPS ? out_hops + (size_t)si * V : nullptr;
+        if (s < 0 || s >= V) {
+            for (int v = lane; v < V; v += SDNR_WAVE) {
+                prow[v] = -1;
+                trow[v] = -1;
+                if (HOPS) hrow[v] = -1;
+            }
+            continue;
+        }
+        for (int w = lane; w < VW; w += SDNR_WAVE) vis[w] = 0u;
+        __syncthreads();
+        if (lane == 0) {
+            vis[s >> 5] = 1u << (s & 31);
+            prow[s] = s;
+            trow[s] = -1;
+            if (HOPS) hrow[s] = 0;
+            ring[0] = make_uint2((uint32_t)s, 0u);
+        }
+        __syncthreads();
+
+        int lsp = 1, bot = 0, gsp = 0;
+        for (;;) {
+            if (lsp == 0) {
+                if (gsp == 0) break;
+                const int n = gsp < kRing / 2 ? gsp : kRing / 2;
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                bot = (bot - n) & (kRing - 1);
+                for (int i = lane; i < n; i += SDNR_WAVE)
+                    ring[(bot + i) & (kRing - 1)] = spill[gsp - n + i];
+                gsp -= n;
+                lsp = n;
+            }
+            const int kk = lsp < K ? lsp : K;
+            uint2 me = ring[(bot + lsp - 1 - lane) & (kRing - 1)];
+            me.x = lane < kk ? me.x : 0u;
+            me.y = lane < kk ? me.y : 0u;
+            int x[J];
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const int slot = j * R + sub;
+                const int u = __shfl((int)me.x, slot);             // slot >= kk: vertex 0
+                x[j] = col[u * W + pos];
+            }
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const int ok = -(int)(((j * R + sub) < kk) & (pos < W));
+                x[j] = (x[j] & ok) | ~ok;
+            }
+            uint64_t m[J];
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const int xi = x[j] & 0x7FFFFFFF;
+                const uint32_t w = vis[(xi >> 5) & ((x[j] >> 31) ^ -1)];
+                m[j] = __ballot((x[j] >= 0) & (((w >> (xi & 31)) & 1u) == 0u));
+            }
+            int jstar = J;
+#pragma unroll
+            for (int j = J - 1; j >= 0; --j)
+                if (m[j] != 0) jstar = j;
+            if (jstar == J) {
+                lsp -= kk;
+                continue;
+            }
+            uint64_t mj = 0;
+            int vv = -1;
+#pragma unroll
+            for (int j = 0; j < J; ++j)
+                if (j == jstar) {
+                    mj = m[j];
+                    vv = x[j];
+                }
+            const int sstar = (__ffsll((unsigned long long)mj) - 1) / LPR;   // sub-slot
+            const int istar = jstar * R + sstar;
+            const uint64_t mm = mj & (lowmask << (sstar * LPR));
+            const int eu = read_lane((int)me.x, istar);
+            const uint32_t ed = (uint32_t)read_lane((int)me.y, istar);
+            lsp -= istar + 1;
+            const int cnt = __popcll(mm);
+            if (lsp + cnt > kRing) {
+                for (int i = lane; i < kRing / 2; i += SDNR_WAVE)
+                    spill[gsp + i] = ring[(bot + i) & (kRing - 1)];
+                gsp += kRing / 2;
+                bot = (bot + kRing / 2) & (kRing - 1);
+                lsp -= kRing / 2;
+            }
+            if ((mm >> lane) & 1ull) {
+                const int rank = lanes_below(mm);
+                atomicOr(&vis[vv >> 5], 1u << (vv & 31));
+                prow[vv] = eu;
+                trow[vv] = port[eu * W + pos];
+                if (HOPS) hrow[vv] = (int)ed + 1;
+                ring[(bot + lsp + rank) & (kRing - 1)] = make_uint2((uint32_t)vv, ed + 1u);
+            }
+            lsp += cnt;
+        }
+        __syncthreads();
+        for (int v = lane; v < V; v += SDNR_WAVE) {
+            if (((vis[v >> 5] >> (v & 31)) & 1u) == 0u) {
+                prow[v] = -1;
+                trow[v] = -1;
+                if (HOPS) hrow[v] = -1;
+            }
         }
         __syncthreads();
     }
@@ -977,6 +1122,23 @@ static int dfs_coop_kw()
     return 4;
 }
 
+// waves per source of the counted-pop kernel: SDNROUTE_DFS_COUNT_WAVES=2|4|6
+static int dfs_count_waves()
+{
+    if (const char *f = getenv("SDNROUTE_DFS_COUNT_WAVES")) {
+        const int k = atoi(f);
+        if (k == 2 || k == 4 || k == 6) return k;
+    }
+    return 4;
+}
+
+// SDNROUTE_DFS_PACKED=0 disables the lane-packed large-graph kernel
+static bool packed_ok()
+{
+    const char *f = getenv("SDNROUTE_DFS_PACKED");
+    return !(f && !strcmp(f, "0"));
+}
+
 // pops checked per batch: wide rows make each leaf pop expensive, so batch
 // deeper; SDNROUTE_DFS_BATCH=1|4|8|16 overrides (tuning / tests)
 static int dfs_batch_depth(const sdnr_ctx *ctx)
@@ -1041,16 +1203,22 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         if (cpc < 1) cpc = 1;
         int cgrid = (int)((size_t)ctx->num_cus * cpc);
         if (cgrid > nsrc) cgrid = nsrc;
-#define SDNR_COUNT(H_)                                                                       \
+        const int nw = dfs_count_waves();
+#define SDNR_COUNT(N_, H_)                                                                   \
     do {                                                                                     \
-        auto k = dfs_count_kernel<4, H_>;                                                    \
+        auto k = dfs_count_kernel<N_, H_>;                                                   \
         allow_full_lds(k);                                                                   \
-        hipLaunchKernelGGL(k, dim3(cgrid), dim3(256), cl, ctx->stream, V, ctx->adj16,        \
+        hipLaunchKernelGGL(k, dim3(cgrid), dim3(N_ * 64), cl, ctx->stream, V, ctx->adj16,    \
                            ctx->radj16, ctx->deg2, ctx->row_ptr, ctx->port, d_src, nsrc,     \
                            d_parent, d_port, d_hops);                                        \
     } while (0)
-        if (hops) SDNR_COUNT(true);
-        else SDNR_COUNT(false);
+        if (nw == 2) {
+            if (hops) SDNR_COUNT(2, true); else SDNR_COUNT(2, false);
+        } else if (nw == 6) {
+            if (hops) SDNR_COUNT(6, true); else SDNR_COUNT(6, false);
+        } else {
+            if (hops) SDNR_COUNT(4, true); else SDNR_COUNT(4, false);
+        }
 #undef SDNR_COUNT
     } else if (coop) {
         const size_t cl = dfs_lds_bytes_coop(V);
@@ -1062,6 +1230,25 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         const int kw = dfs_coop_kw();
         if (hops) launch_coop<true>(kw, cgrid, cl, ctx->stream, V, ctx->adj16, a);
         else launch_coop<false>(kw, cgrid, cl, ctx->stream, V, ctx->adj16, a);
+    } else if (!small && ell && ctx->W <= 32 && packed_ok()) {
+        // lanes per row = next power of two >= W
+        const int lpr = ctx->W <= 8 ? 8 : (ctx->W <= 16 ? 16 : 32);
+#define SDNR_PACKED(L_, J_, H_)                                                              \
+    do {                                                                                     \
+        auto k = dfs_global_packed_kernel<L_, J_, H_>;                                       \
+        allow_full_lds(k);                                                                   \
+        hipLaunchKernelGGL(k, dim3(grid), dim3(64), lds, ctx->stream, V, ctx->W,             \
+                           ctx->ell_col, ctx->ell_port, d_src, nsrc, d_parent, d_port,       \
+                           d_hops, spill);                                                   \
+    } while (0)
+        if (lpr == 8) {
+            if (hops) SDNR_PACKED(8, 2, true); else SDNR_PACKED(8, 2, false);
+        } else if (lpr == 16) {
+            if (hops) SDNR_PACKED(16, 4, true); else SDNR_PACKED(16, 4, false);
+        } else {
+            if (hops) SDNR_PACKED(32, 8, true); else SDNR_PACKED(32, 8, false);
+        }
+#undef SDNR_PACKED
     } else if (narrow) {
         const int K = dfs_batch_depth(ctx);
         if (ell && hops) launch_batch_k<true, true>(K, small, grid, lds, ctx->stream, a);

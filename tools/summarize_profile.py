@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Summarize a tools/profile_gpu.sh output directory into profiles/.
+
+    python tools/summarize_profile.py gpurun_out/prof_TAG profiles/r01_TAG
+
+Writes <out>_kernel_stats.csv (rocprofv3 --kernel-trace --stats, verbatim),
+<out>_pmc.json (per-dispatch means of every PMC counter, per kernel) and
+<out>_summary.md (human-readable, with the HBM traffic derived as
+MI355X_MICROARCH.md prescribes: FETCH_SIZE x 2 on gfx950 for wide streaming
+reads, WRITE_SIZE as reported, both in KiB per dispatch).
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+
+def main(src, out):
+    os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
+    stats = os.path.join(src, "trace", "run_kernel_stats.csv")
+    if os.path.exists(stats):
+        shutil.copy(stats, out + "_kernel_stats.csv")
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    meta = {}
+    for f in sorted(glob.glob(os.path.join(src, "pmc*", "run_counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"]
+            per[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            meta[k] = {x: r[x] for x in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size",
+                                        "VGPR_Count", "SGPR_Count", "Scratch_Size")}
+    pmc = {k: {"meta": meta[k], "counters": {c: sum(v) / len(v) for c, v in cs.items()},
+               "dispatches": max(len(v) for v in cs.values())}
+           for k, cs in per.items()}
+    json.dump(pmc, open(out + "_pmc.json", "w"), indent=1, sort_keys=True)
+    lines = ["# rocprofv3 summary: %s" % os.path.basename(out), ""]
+    if os.path.exists(stats):
+        lines += ["## kernel trace (--kernel-trace --stats)", "", "| kernel | calls | avg us | min us | max us |",
+                  "|---|---|---|---|---|"]
+        for r in csv.DictReader(open(stats)):
+            lines.append("| %s | %s | %.1f | %.1f | %.1f |" % (
+                r["Name"][:90], r["Calls"], float(r["AverageNs"]) / 1e3,
+                float(r["MinNs"]) / 1e3, float(r["MaxNs"]) / 1e3))
+    for k, d in pmc.items():
+        if "rocclr" in k:
+            continue
+        c = d["counters"]
+        lines += ["", "## %s" % k[:120], "", "launch: %s" % d["meta"], ""]
+        for name in sorted(c):
+            lines.append("- %s: %.4g per dispatch" % (name, c[name]))
+        if "FETCH_SIZE" in c or "WRITE_SIZE" in c:
+            fetch = c.get("FETCH_SIZE", 0.0)
+            write = c.get("WRITE_SIZE", 0.0)
+            lines.append("- HBM traffic per dispatch (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 "
+                         "correction of MI355X_MICROARCH.md): %.1f MB"
+                         % ((2 * fetch + write) * 1024 / 1e6))
+        if "SQ_WAVE_CYCLES" in c:
+            wc = c["SQ_WAVE_CYCLES"]
+            lines.append("- wave-cycle split: wait %.0f%%, issue-stall %.0f%%, active %.0f%%" % (
+                100 * c.get("SQ_WAIT_ANY", 0) / wc, 100 * c.get("SQ_WAIT_INST_ANY", 0) / wc,
+                100 * c.get("SQ_ACTIVE_INST_ANY", 0) / wc))
+    open(out + "_summary.md", "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
