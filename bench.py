@@ -232,7 +232,7 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": "dfs_lds_kernel" if args.mode == "dfs" else "msbfs+nexthop",
+            "kernel": ctx.last_kernel(),
             "kernel_ms": kern_ms, "bytes_per_launch": bytes_launch,
         },
         "switch_pair_routes_per_s": float(S) * V / (ms_per_step / 1e3),

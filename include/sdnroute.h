@@ -120,6 +120,10 @@ int sdnr_apsp(sdnr_ctx *ctx, uint16_t *dist, uint32_t flags);
  * made with SDNR_TIMING (waits for that call to finish). */
 int sdnr_last_kernel_ms(sdnr_ctx *ctx, float *ms);
 
+/* Name of the kernel variant the last table call launched on this context
+ * (e.g. "dfs_count_kernel<4>"; "" before the first call). */
+const char *sdnr_last_kernel(const sdnr_ctx *ctx);
+
 #ifdef __cplusplus
 }
 #endif

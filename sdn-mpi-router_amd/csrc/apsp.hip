@@ -150,6 +150,7 @@ int sdnr_launch_apsp(sdnr_ctx *ctx, uint16_t *d_dist)
         if (rc) return rc;
         D = static_cast<uint16_t *>(ctx->scratch);
     }
+    ctx->last_kernel = "apsp_phase{1,2,3}_kernel";
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
     hipLaunchKernelGGL(apsp_init_kernel, dim3(1024), dim3(256), 0, ctx->stream, V, Vp,
                        ctx->row_ptr, ctx->col, D);

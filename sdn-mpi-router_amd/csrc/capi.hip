@@ -391,6 +391,8 @@ int sdnr_apsp(sdnr_ctx *ctx, uint16_t *dist, uint32_t flags)
     return SDNR_OK;
 }
 
+const char *sdnr_last_kernel(const sdnr_ctx *ctx) { return ctx ? ctx->last_kernel : ""; }
+
 int sdnr_last_kernel_ms(sdnr_ctx *ctx, float *ms)
 {
     CHECK_CTX(ctx);

@@ -59,6 +59,7 @@ struct sdnr_ctx {
     // timing of the main kernel(s) of the last SDNR_TIMING call
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
+    const char *last_kernel = "";       // variant launched by the last table call
 };
 
 // Raise a kernel's dynamic-LDS limit; a refusal (e.g. static LDS + bytes >

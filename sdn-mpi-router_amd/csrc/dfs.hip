@@ -1204,6 +1204,8 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         int cgrid = (int)((size_t)ctx->num_cus * cpc);
         if (cgrid > nsrc) cgrid = nsrc;
         const int nw = dfs_count_waves();
+        ctx->last_kernel = nw == 2 ? "dfs_count_kernel<2>" : nw == 6 ? "dfs_count_kernel<6>"
+                                                                    : "dfs_count_kernel<4>";
 #define SDNR_COUNT(N_, H_)                                                                   \
     do {                                                                                     \
         auto k = dfs_count_kernel<N_, H_>;                                                   \
@@ -1228,11 +1230,13 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         int cgrid = (int)((size_t)ctx->num_cus * cpc);
         if (cgrid > nsrc) cgrid = nsrc;
         const int kw = dfs_coop_kw();
+        ctx->last_kernel = "dfs_coop_kernel";
         if (hops) launch_coop<true>(kw, cgrid, cl, ctx->stream, V, ctx->adj16, a);
         else launch_coop<false>(kw, cgrid, cl, ctx->stream, V, ctx->adj16, a);
     } else if (!small && ell && ctx->W <= 32 && packed_ok()) {
         // lanes per row = next power of two >= W
         const int lpr = ctx->W <= 8 ? 8 : (ctx->W <= 16 ? 16 : 32);
+        ctx->last_kernel = "dfs_global_packed_kernel";
 #define SDNR_PACKED(L_, J_, H_)                                                              \
     do {                                                                                     \
         auto k = dfs_global_packed_kernel<L_, J_, H_>;                                       \
@@ -1251,11 +1255,13 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
 #undef SDNR_PACKED
     } else if (narrow) {
         const int K = dfs_batch_depth(ctx);
+        ctx->last_kernel = small ? "dfs_lds_batch_kernel" : "dfs_global_batch_kernel";
         if (ell && hops) launch_batch_k<true, true>(K, small, grid, lds, ctx->stream, a);
         else if (ell) launch_batch_k<true, false>(K, small, grid, lds, ctx->stream, a);
         else if (hops) launch_batch_k<false, true>(K, small, grid, lds, ctx->stream, a);
         else launch_batch_k<false, false>(K, small, grid, lds, ctx->stream, a);
     } else {
+        ctx->last_kernel = small ? "dfs_lds_wide_kernel" : "dfs_global_wide_kernel";
         if (hops) launch_wide<true>(small, grid, lds, ctx->stream, a);
         else launch_wide<false>(small, grid, lds, ctx->stream, a);
     }

@@ -164,6 +164,8 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
     SDNR_HIP(hipMemsetAsync(d_dist, 0xFF, (size_t)ndst * V * sizeof(uint16_t), ctx->stream));
     const size_t lds = (size_t)V * 3 * sizeof(uint64_t);
+    ctx->last_kernel = lds <= 150 * 1024 ? "msbfs_lds_kernel+nexthop_kernel"
+                                         : "msbfs_level_kernel+nexthop_kernel";
     if (lds <= 150 * 1024) {
         auto k = msbfs_lds_kernel;
         if (lds > 64 * 1024) sdnr_allow_lds(reinterpret_cast<const void *>(k), lds);

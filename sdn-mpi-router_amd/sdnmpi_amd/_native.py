@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = (
     "sdnr_abi_version", "sdnr_last_error", "sdnr_device_count", "sdnr_create",
     "sdnr_destroy", "sdnr_set_stream", "sdnr_synchronize", "sdnr_graph_upload",
     "sdnr_graph_info", "sdnr_dfs_tables", "sdnr_shortest_tables", "sdnr_apsp",
-    "sdnr_last_kernel_ms",
+    "sdnr_last_kernel_ms", "sdnr_last_kernel",
 )
 
 
@@ -72,6 +72,7 @@ def _bind(L):
         "sdnr_shortest_tables": ([vp, vp, i32, vp, vp, vp, u32], c_int),
         "sdnr_apsp": ([vp, vp, u32], c_int),
         "sdnr_last_kernel_ms": ([vp, ctypes.POINTER(ctypes.c_float)], c_int),
+        "sdnr_last_kernel": ([vp], ctypes.c_char_p),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -222,6 +223,9 @@ class Context(object):
     def apsp_device(self, dist_ptr, timing=False):
         flags = DEVICE_PTRS | (TIMING if timing else 0)
         _check(self._lib.sdnr_apsp(self._h, ctypes.c_void_p(dist_ptr), flags))
+
+    def last_kernel(self):
+        return self._lib.sdnr_last_kernel(self._h).decode()
 
     def last_kernel_ms(self):
         ms = ctypes.c_float()
