@@ -60,10 +60,10 @@ static void free_graph(sdnr_ctx *c)
     }
     if (c->radj16 && c->radj_owned) (void)hipFree(c->radj16);
     if (c->adj16) (void)hipFree(c->adj16);
-    if (c->deg2) (void)hipFree(c->deg2);
+    if (c->deg32) (void)hipFree(c->deg32);
     c->adj16 = nullptr;
     c->radj16 = nullptr;
-    c->deg2 = nullptr;
+    c->deg32 = nullptr;
     c->radj_owned = false;
     c->V = -1;
     c->E = 0;
@@ -229,10 +229,10 @@ int sdnr_graph_upload(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_pt
         const size_t rows = ((size_t)V + 1) * SDNR_WAVE;
         std::vector<uint16_t> a16(rows, (uint16_t)V), r16(rows, (uint16_t)V);
         std::vector<int32_t> indeg((size_t)V + 1, 0);
-        std::vector<uint32_t> d2(((size_t)V + 2) / 2 + 4, 0u);
+        std::vector<uint32_t> d32((size_t)V + 1, 0u);
         for (int32_t u = 0; u < V; ++u) {
             const int32_t d = row_ptr[u + 1] - row_ptr[u];
-            d2[(size_t)u >> 1] |= (uint32_t)d << ((u & 1) * 16);
+            d32[(size_t)u] = (uint32_t)d;
             for (int32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) {
                 a16[(size_t)u * SDNR_WAVE + (e - row_ptr[u])] = (uint16_t)col[e];
                 indeg[col[e]]++;
@@ -254,9 +254,9 @@ int sdnr_graph_upload(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_pt
         if (he == hipSuccess)
             he = hipMemcpyAsync(ctx->adj16, a16.data(), rows * 2, hipMemcpyHostToDevice, ctx->stream);
         if (he == hipSuccess && maxin <= SDNR_WAVE) {
-            he = hipMalloc(reinterpret_cast<void **>(&ctx->deg2), d2.size() * 4);
+            he = hipMalloc(reinterpret_cast<void **>(&ctx->deg32), d32.size() * 4);
             if (he == hipSuccess)
-                he = hipMemcpyAsync(ctx->deg2, d2.data(), d2.size() * 4, hipMemcpyHostToDevice,
+                he = hipMemcpyAsync(ctx->deg32, d32.data(), d32.size() * 4, hipMemcpyHostToDevice,
                                     ctx->stream);
             if (he == hipSuccess && sym) {
                 ctx->radj16 = ctx->adj16;

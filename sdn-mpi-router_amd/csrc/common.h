@@ -47,7 +47,7 @@ struct sdnr_ctx {
     int32_t *ell_col = nullptr, *ell_port = nullptr;
     uint16_t *adj16 = nullptr;          // (V+1) rows x 64 u16, sentinel V (V < 65535)
     uint16_t *radj16 = nullptr;         // in-neighbour rows, same layout (== adj16 if symmetric)
-    uint32_t *deg2 = nullptr;           // out-degrees of 0..V as u16 pairs
+    uint32_t *deg32 = nullptr;          // out-degrees of 0..V (sentinel V: 0)
     bool radj_owned = false;
 
     // grow-only device scratch / staging

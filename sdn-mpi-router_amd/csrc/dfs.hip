@@ -725,20 +725,32 @@ __global__ __launch_bounds__(NW * 64) void dfs_coop_kernel(
 // are split round-robin over the waves; barrier A separates the visited
 // gathers from the marks, barrier B publishes the push.
 // ---------------------------------------------------------------------------
+#ifdef SDNR_STAMPS
+// diagnostic build only: cycles per phase of the counted-pop loop, summed
+// over every source by wave 0 of each workgroup (never in the real kernel)
+__device__ unsigned long long g_stamp[8];
+#define SDNR_STAMP(t) \
+    do { __builtin_amdgcn_sched_barrier(0); \
+         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory"); \
+         __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define SDNR_STAMP(t) do { (void)(t); } while (0)
+#endif
+
 template <int NW, bool HOPS>
 __global__ __launch_bounds__(NW * 64) void dfs_count_kernel(
     int V, const uint16_t *__restrict__ adj, const uint16_t *__restrict__ radj,
-    const uint32_t *__restrict__ deg2, const int32_t *__restrict__ row_ptr,
+    const uint32_t *__restrict__ deg, const int32_t *__restrict__ row_ptr,
     const int32_t *__restrict__ port, const int32_t *__restrict__ src, int nsrc,
     int32_t *__restrict__ out_parent, int32_t *__restrict__ out_port,
     int32_t *__restrict__ out_hops)
 {
+    constexpr int G = 8;                         // child rows in flight per wave
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int VW = (V + 1 + 31) >> 5;            // + sentinel bit V
     const int VWp = (VW + 3) & ~3;
-    const int CW = (V + 2) >> 1;                 // u16 counts of 0..V, in pairs
-    const int CWp = (CW + 3) & ~3;
-    const int SWp = (((V + 1) >> 1) + 3) & ~3;   // u16 stack / depth words
+    const int CWp = (V + 1 + 3) & ~3;            // u32 counts of 0..V
+    const int SWp = (((V + 1) >> 1) + 3) & ~3;   // u16 stack
     uint32_t *vis = lds;
     uint32_t *cnt = vis + VWp;
     uint16_t *stk = reinterpret_cast<uint16_t *>(cnt + CWp);
@@ -746,6 +758,10 @@ __global__ __launch_bounds__(NW * 64) void dfs_count_kernel(
     uint16_t *dep = reinterpret_cast<uint16_t *>(ps + V);
     const int lane = lane_id();
     const int w = threadIdx.x >> 6;
+    unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0, t5 = 0;   // stamps (diag)
+#ifdef SDNR_STAMPS
+    unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
+#endif
 
     for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
         const int s = uniform(src[si]);
@@ -761,7 +777,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_count_kernel(
             continue;
         }
         for (int i = threadIdx.x; i < VW; i += blockDim.x) vis[i] = 0u;
-        for (int i = threadIdx.x; i < CW; i += blockDim.x) cnt[i] = deg2[i];
+        for (int i = threadIdx.x; i <= V; i += blockDim.x) cnt[i] = deg[i];
         __syncthreads();
         if (threadIdx.x == 0) {
             vis[s >> 5] |= 1u << (s & 31);
@@ -772,13 +788,14 @@ __global__ __launch_bounds__(NW * 64) void dfs_count_kernel(
         }
         if (w == 0) {                            // s is visited: its in-neighbours lose one
             const int r = radj[(size_t)s * 64 + lane];
-            if (r != V) atomicSub(&cnt[r >> 1], (r & 1) ? 0x10000u : 1u);
+            if (r != V) atomicSub(&cnt[r], 1u);
         }
         __syncthreads();
 
         int sp = 1;
         int pu = -1, xpre = V;                   // speculatively loaded row of pu
         for (;;) {
+            SDNR_STAMP(t0);
             // ---- skip leaf pops, 64 stack slots per step
             uint64_t m = 0;
             int e = V;
@@ -787,8 +804,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_count_kernel(
                 const int at = sp - 1 - lane;
                 e = stk[at < 0 ? 0 : at];
                 e = lane < kk ? e : V;
-                const uint32_t c = (cnt[e >> 1] >> ((e & 1) << 4)) & 0xFFFFu;
-                m = __ballot(c != 0u);
+                m = __ballot(cnt[e] != 0u);
                 if (m) break;
                 sp -= kk;
             }
@@ -796,6 +812,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_count_kernel(
             const int first = __ffsll((unsigned long long)m) - 1;
             const int u = read_lane(e, first);
             sp -= first + 1;
+            SDNR_STAMP(t1);
             // ---- the non-leaf pop: forward row (usually prefetched: the
             // top of the stack is the previous push's largest child), visited gather
             const int x = (u == pu) ? xpre : (int)adj[(size_t)u * 64 + lane];
@@ -807,22 +824,25 @@ __global__ __launch_bounds__(NW * 64) void dfs_count_kernel(
             xpre = adj[(size_t)pu * 64 + lane];
             int du = 0;
             if (HOPS) du = uniform((int)dep[u]);
+            SDNR_STAMP(t2);
             __syncthreads();                     // A: gathers before marks
+            SDNR_STAMP(t3);
             if (w == 0 && fresh) {
                 atomicOr(&vis[x >> 5], 1u << (x & 31));
                 ps[x] = (uint32_t)u | ((uint32_t)lane << 16);
                 if (HOPS) dep[x] = (uint16_t)(du + 1);
                 stk[sp + rank] = (uint16_t)x;
             }
-            // ---- children decrement their in-neighbours' counts
+            // ---- children decrement their in-neighbours' counts; child j
+            // (ascending) belongs to wave j % NW, up to G rows in flight
             uint64_t mine = __ballot(fresh && (rank % NW) == w);
-            while (mine) {                       // all of a wave's rows in flight together
-                constexpr int G = 64 / NW < 16 ? 64 / NW : 16;
+            int n = __popcll(mine);
+            while (n > 0) {
                 int r[G];
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
-                    int v = V;
-                    if (mine) {
+                    int v = V;                   // past n: the all-sentinel row
+                    if (g < n) {
                         v = read_lane(x, __ffsll((unsigned long long)mine) - 1);
                         mine &= mine - 1;
                     }
@@ -830,10 +850,21 @@ __global__ __launch_bounds__(NW * 64) void dfs_count_kernel(
                 }
 #pragma unroll
                 for (int g = 0; g < G; ++g)
-                    if (r[g] != V) atomicSub(&cnt[r[g] >> 1], (r[g] & 1) ? 0x10000u : 1u);
+                    if (g < n && r[g] != V) atomicSub(&cnt[r[g]], 1u);
+                n -= G;
             }
             sp += __popcll(mm);
+            SDNR_STAMP(t4);
             __syncthreads();                     // B: publish the push
+            SDNR_STAMP(t5);
+#ifdef SDNR_STAMPS
+            acc[0] += t1 - t0;
+            acc[1] += t2 - t1;
+            acc[2] += t3 - t2;
+            acc[3] += t4 - t3;
+            acc[4] += t5 - t4;
+            acc[5] += 1;
+#endif
         }
         __syncthreads();
 
@@ -855,6 +886,10 @@ __global__ __launch_bounds__(NW * 64) void dfs_count_kernel(
         }
         __syncthreads();
     }
+#ifdef SDNR_STAMPS
+    if (threadIdx.x == 0)
+        for (int k = 0; k < 6; ++k) atomicAdd(&g_stamp[k], acc[k]);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1077,7 +1112,7 @@ void launch_wide(bool small, int grid, size_t lds, hipStream_t st, const DfsArgs
 static size_t dfs_lds_bytes_count(int V, bool hops)
 {
     const size_t VWp = (size_t)((((V + 1 + 31) >> 5) + 3) & ~3);
-    const size_t CWp = (size_t)((((V + 2) >> 1) + 3) & ~3);
+    const size_t CWp = (size_t)((V + 1 + 3) & ~3);
     const size_t SWp = (size_t)((((V + 1) >> 1) + 3) & ~3);
     return align16(4 * (VWp + CWp + SWp) + 4 * (size_t)V + (hops ? 2 * (size_t)V : 0));
 }
@@ -1121,6 +1156,17 @@ static int dfs_coop_kw()
     }
     return 4;
 }
+
+#ifdef SDNR_STAMPS
+extern "C" int sdnr_debug_stamps(unsigned long long *out6)
+{
+    if (hipMemcpyFromSymbol(out6, HIP_SYMBOL(g_stamp), 6 * sizeof(unsigned long long)) !=
+        hipSuccess)
+        return -5;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof z) == hipSuccess ? 0 : -5;
+}
+#endif
 
 // waves per source of the counted-pop kernel: SDNROUTE_DFS_COUNT_WAVES=2|4|6
 static int dfs_count_waves()
@@ -1211,7 +1257,7 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         auto k = dfs_count_kernel<N_, H_>;                                                   \
         allow_full_lds(k);                                                                   \
         hipLaunchKernelGGL(k, dim3(cgrid), dim3(N_ * 64), cl, ctx->stream, V, ctx->adj16,    \
-                           ctx->radj16, ctx->deg2, ctx->row_ptr, ctx->port, d_src, nsrc,     \
+                           ctx->radj16, ctx->deg32, ctx->row_ptr, ctx->port, d_src, nsrc,     \
                            d_parent, d_port, d_hops);                                        \
     } while (0)
         if (nw == 2) {
