@@ -69,7 +69,9 @@ int sdnr_destroy(sdnr_ctx *ctx);
  * restores the context's own stream. */
 int sdnr_set_stream(sdnr_ctx *ctx, void *hip_stream);
 
-/* Wait for all work queued on the context's stream. */
+/* Wait for all work queued on the context's stream.  Also reports (as
+ * SDNR_ERR_HIP) a kernel whose bounded internal wait ran out -- the
+ * kernels never spin unboundedly; that only happens on a bug. */
 int sdnr_synchronize(sdnr_ctx *ctx);
 
 /* Upload the switch graph (host buffers).  Replaces the graph state that

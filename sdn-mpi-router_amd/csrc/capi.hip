@@ -33,6 +33,19 @@ int sdnr_hip_fail(hipError_t e, const char *what)
     return sdnr_fail(code, "%s: %s", what, hipGetErrorString(e));
 }
 
+// A kernel whose bounded spin ran out sets *d_err instead of hanging; report
+// it once (and clear it) after the work has been waited for.
+int sdnr_check_watchdog(sdnr_ctx *ctx)
+{
+    int h = 0;
+    SDNR_HIP(hipMemcpy(&h, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (h) {
+        SDNR_HIP(hipMemset(ctx->d_err, 0, sizeof(int)));
+        return sdnr_fail(SDNR_ERR_HIP, "kernel watchdog tripped (code %d): results invalid", h);
+    }
+    return SDNR_OK;
+}
+
 int sdnr_reserve(void **buf, size_t *cur, size_t need)
 {
     if (need <= *cur && *buf) return SDNR_OK;
@@ -125,6 +138,8 @@ int sdnr_create(int device, sdnr_ctx **out)
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&c->d_err), sizeof(int));
+    if (e == hipSuccess) e = hipMemset(c->d_err, 0, sizeof(int));
     if (e != hipSuccess) {
         delete c;
         return sdnr_hip_fail(e, "sdnr_create");
@@ -142,6 +157,7 @@ int sdnr_destroy(sdnr_ctx *ctx)
     free_graph(ctx);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->stage) (void)hipFree(ctx->stage);
+    if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
@@ -161,7 +177,7 @@ int sdnr_synchronize(sdnr_ctx *ctx)
     CHECK_CTX(ctx);
     SDNR_HIP(hipSetDevice(ctx->device));
     SDNR_HIP(hipStreamSynchronize(ctx->stream));
-    return SDNR_OK;
+    return sdnr_check_watchdog(ctx);
 }
 
 int sdnr_graph_upload(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_ptr,
@@ -345,7 +361,7 @@ int sdnr_dfs_tables(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc, int32_t *pa
     SDNR_HIP(hipMemcpyAsync(port, d_prt, rows * 4, hipMemcpyDeviceToHost, ctx->stream));
     if (hops) SDNR_HIP(hipMemcpyAsync(hops, d_hop, rows * 4, hipMemcpyDeviceToHost, ctx->stream));
     SDNR_HIP(hipStreamSynchronize(ctx->stream));
-    return SDNR_OK;
+    return sdnr_check_watchdog(ctx);
 }
 
 int sdnr_shortest_tables(sdnr_ctx *ctx, const int32_t *dst, int32_t ndst, uint16_t *dist,

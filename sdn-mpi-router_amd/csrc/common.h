@@ -60,6 +60,7 @@ struct sdnr_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     const char *last_kernel = "";       // variant launched by the last table call
+    int *d_err = nullptr;               // kernel watchdog word (0 = ok)
 };
 
 // Raise a kernel's dynamic-LDS limit; a refusal (e.g. static LDS + bytes >
@@ -75,6 +76,7 @@ inline void sdnr_allow_lds(const void *fn, size_t bytes)
 int sdnr_fail(int code, const char *fmt, ...);
 int sdnr_hip_fail(hipError_t e, const char *what);
 int sdnr_reserve(void **buf, size_t *cur, size_t need);
+int sdnr_check_watchdog(sdnr_ctx *ctx);   // after a stream sync
 
 #define SDNR_HIP(call)                                           \
     do {                                                         \

@@ -1032,6 +1032,191 @@ __global__ __launch_bounds__(64) void dfs_global_packed_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Asynchronous counted pops (the k=48 headline kernel).
+//
+// Same counts as dfs_count_kernel, one observation further: a count may be
+// STALE HIGH without breaking exactness.  If the skip stops at an entry whose
+// count still includes a neighbour visited a moment ago, the row check finds
+// no fresh child and the entry is popped as the leaf pop it is.  A count is
+// never low (a decrement is published only after its mark).  So the
+// decrements need not finish before the next pop: wave 0 runs the search
+// chain alone -- skip, row, visited gather, push -- with no barrier, and
+// publishes each push's children into an LDS ring; waves 1..NW-1 drain the
+// ring (child j belongs to worker 1 + j % (NW-1)), load the children's
+// in-rows and ds_sub the counts.  Hand-off inside the workgroup: ring writes,
+// release fence, relaxed store of the published count; workers acquire-load
+// it.  Back-pressure keeps the ring from overrunning the slowest worker.
+// Every spin is bounded; the bound only trips on a bug, and then sets the
+// error word instead of hanging the GPU.
+// ---------------------------------------------------------------------------
+template <int NW, bool HOPS>
+__global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
+    int V, const uint16_t *__restrict__ adj, const uint16_t *__restrict__ radj,
+    const uint32_t *__restrict__ deg, const int32_t *__restrict__ row_ptr,
+    const int32_t *__restrict__ port, const int32_t *__restrict__ src, int nsrc,
+    int32_t *__restrict__ out_parent, int32_t *__restrict__ out_port,
+    int32_t *__restrict__ out_hops, int *__restrict__ err)
+{
+    static_assert(NW >= 2, "wave 0 searches, the others decrement");
+    constexpr int S = NW - 1;                    // workers
+    constexpr int RING = 512;                    // children in flight (u16)
+    constexpr int G = 8;                         // rows in flight per worker
+    constexpr unsigned kSpin = 1u << 22;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int VW = (V + 1 + 31) >> 5;
+    const int VWp = (VW + 3) & ~3;
+    const int CWp = (V + 1 + 3) & ~3;
+    const int SWp = (((V + 1) >> 1) + 3) & ~3;
+    uint32_t *vis = lds;
+    uint32_t *cnt = vis + VWp;
+    uint16_t *stk = reinterpret_cast<uint16_t *>(cnt + CWp);
+    uint32_t *ps = cnt + CWp + SWp;
+    uint16_t *dep = reinterpret_cast<uint16_t *>(ps + V);
+    uint16_t *ring = reinterpret_cast<uint16_t *>(ps + V + (HOPS ? ((V + 1) >> 1) : 0));
+    int *ctl = reinterpret_cast<int *>(ring + RING);   // [0] published [1] done [2+k] consumed
+    const int lane = lane_id();
+    const int w = threadIdx.x >> 6;
+
+    for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
+        const int s = uniform(src[si]);
+        int32_t *prow = out_parent + (size_t)si * V;
+        int32_t *trow = out_port + (size_t)si * V;
+        int32_t *hrow = HOPS ? out_hops + (size_t)si * V : nullptr;
+        if (s < 0 || s >= V) {
+            for (int v = threadIdx.x; v < V; v += blockDim.x) {
+                prow[v] = -1;
+                trow[v] = -1;
+                if (HOPS) hrow[v] = -1;
+            }
+            continue;
+        }
+        for (int i = threadIdx.x; i < VW; i += blockDim.x) vis[i] = 0u;
+        for (int i = threadIdx.x; i <= V; i += blockDim.x) cnt[i] = deg[i];
+        if (threadIdx.x < 2 + S) ctl[threadIdx.x] = 0;
+        __syncthreads();
+
+        if (w == 0) {
+            // ------------------------------------------------ the search
+            if (lane == 0) {
+                vis[s >> 5] |= 1u << (s & 31);
+                vis[V >> 5] |= 1u << (V & 31);
+                ps[s] = (uint32_t)s;
+                if (HOPS) dep[s] = 0;
+                stk[0] = (uint16_t)s;
+                ring[0] = (uint16_t)s;           // s's in-neighbours lose one
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_store(&ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            int pub = 1, sp = 1, pu = -1, xpre = V;
+            for (;;) {
+                uint64_t m = 0;
+                int e = V;
+                while (sp > 0) {
+                    const int kk = sp < 64 ? sp : 64;
+                    const int at = sp - 1 - lane;
+                    e = stk[at < 0 ? 0 : at];
+                    e = lane < kk ? e : V;
+                    const uint32_t c = __hip_atomic_load(&cnt[e], __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+                    m = __ballot(c != 0u);
+                    if (m) break;
+                    sp -= kk;
+                }
+                if (!m) break;
+                const int first = __ffsll((unsigned long long)m) - 1;
+                const int u = read_lane(e, first);
+                sp -= first + 1;
+                const int x = (u == pu) ? xpre : (int)adj[(size_t)u * 64 + lane];
+                const uint32_t wv = vis[x >> 5];
+                const bool fresh = ((wv >> (x & 31)) & 1u) == 0u;
+                const uint64_t mm = __ballot(fresh);
+                if (mm == 0) continue;           // stale count: a leaf pop after all
+                const int c = __popcll(mm);
+                const int rank = lanes_below(mm);
+                pu = read_lane(x, highest_lane(mm));
+                xpre = adj[(size_t)pu * 64 + lane];
+                int du = 0;
+                if (HOPS) du = uniform((int)dep[u]);
+                // back-pressure: ring slots below every worker's progress are free
+                for (unsigned spin = 0;; ++spin) {
+                    int lo = 0x7FFFFFFF;
+#pragma unroll
+                    for (int k = 0; k < S; ++k)
+                        lo = min(lo, __hip_atomic_load(&ctl[2 + k], __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_WORKGROUP));
+                    if (pub + c - lo <= RING) break;
+                    if (spin > kSpin) {
+                        if (lane == 0) atomicOr(err, 1);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (fresh) {
+                    atomicOr(&vis[x >> 5], 1u << (x & 31));
+                    ps[x] = (uint32_t)u | ((uint32_t)lane << 16);
+                    if (HOPS) dep[x] = (uint16_t)(du + 1);
+                    stk[sp + rank] = (uint16_t)x;
+                    ring[(pub + rank) & (RING - 1)] = (uint16_t)x;
+                }
+                pub += c;
+                sp += c;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) __hip_atomic_store(&ctl[0], pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_store(&ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+            // ------------------------------------------------ the decrements
+            int j = w - 1;                       // next child index of this worker
+            for (unsigned spin = 0;;) {
+                const int P = __hip_atomic_load(&ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (j >= P) {
+                    if (__hip_atomic_load(&ctl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) &&
+                        j >= __hip_atomic_load(&ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))
+                        break;
+                    if (++spin > kSpin) {
+                        if (lane == 0) atomicOr(err, 2);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                spin = 0;
+                const int n = (P - j + S - 1) / S < G ? (P - j + S - 1) / S : G;
+                const int mine = lane < n ? (int)ring[(j + lane * S) & (RING - 1)] : V;
+                int r[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) r[g] = radj[(size_t)read_lane(mine, g) * 64 + lane];
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    if (g < n && r[g] != V) atomicSub(&cnt[r[g]], 1u);
+                j += n * S;
+                if (lane == 0) __hip_atomic_store(&ctl[2 + w - 1], j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        __syncthreads();
+
+        for (int v = threadIdx.x; v < V; v += blockDim.x) {
+            int p = -1, pt = -1, h = -1;
+            if ((vis[v >> 5] >> (v & 31)) & 1u) {
+                const uint32_t xx = ps[v];
+                p = (int)(xx & 0xFFFFu);
+                if (v == s) {
+                    h = 0;
+                } else {
+                    pt = port[row_ptr[p] + (int)(xx >> 16)];
+                    h = HOPS ? (int)dep[v] : 0;
+                }
+            }
+            prow[v] = p;
+            trow[v] = pt;
+            if (HOPS) hrow[v] = h;
+        }
+        __syncthreads();
+    }
+}
+
 template <typename Kern>
 void allow_full_lds(Kern kernel)
 {
@@ -1117,6 +1302,15 @@ static size_t dfs_lds_bytes_count(int V, bool hops)
     return align16(4 * (VWp + CWp + SWp) + 4 * (size_t)V + (hops ? 2 * (size_t)V : 0));
 }
 
+static size_t dfs_lds_bytes_async(int V, bool hops)
+{
+    const size_t VWp = (size_t)((((V + 1 + 31) >> 5) + 3) & ~3);
+    const size_t CWp = (size_t)((V + 1 + 3) & ~3);
+    const size_t SWp = (size_t)((((V + 1) >> 1) + 3) & ~3);
+    return align16(4 * (VWp + CWp + SWp) + 4 * (size_t)V +
+                   (hops ? 4 * (size_t)((V + 1) >> 1) : 0) + 2 * 512 + 4 * 16);
+}
+
 static size_t dfs_lds_bytes_coop(int V)
 {
     const size_t VWp = (size_t)((((V + 1 + 31) >> 5) + 3) & ~3);
@@ -1168,6 +1362,16 @@ extern "C" int sdnr_debug_stamps(unsigned long long *out6)
 }
 #endif
 
+// waves per source of the asynchronous kernel: SDNROUTE_DFS_ASYNC_WAVES=2|3|4
+static int dfs_async_waves()
+{
+    if (const char *f = getenv("SDNROUTE_DFS_ASYNC_WAVES")) {
+        const int k = atoi(f);
+        if (k == 2 || k == 3 || k == 4) return k;
+    }
+    return 4;
+}
+
 // waves per source of the counted-pop kernel: SDNROUTE_DFS_COUNT_WAVES=2|4|6
 static int dfs_count_waves()
 {
@@ -1212,7 +1416,8 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
     // debug/test knob: SDNROUTE_DFS_STRATEGY=lds|global forces a strategy
     if (const char *f = getenv("SDNROUTE_DFS_STRATEGY")) {
         if (!strcmp(f, "global")) small = false;
-        else if ((!strcmp(f, "lds") || !strcmp(f, "coop") || !strcmp(f, "count")) && V < 65536 &&
+        else if ((!strcmp(f, "lds") || !strcmp(f, "coop") || !strcmp(f, "count") ||
+                  !strcmp(f, "async")) && V < 65536 &&
                  small_b <= SDNR_MAX_LDS_PER_BLOCK)
             small = true;
     }
@@ -1238,11 +1443,40 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
     const char *force = getenv("SDNROUTE_DFS_STRATEGY");
     const bool count_ok = ctx->adj16 != nullptr && ctx->radj16 != nullptr && V < 65535 &&
                           dfs_lds_bytes_count(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;
-    const bool count = count_ok && (force ? !strcmp(force, "count") : small);
+    const bool async_ok = count_ok && dfs_lds_bytes_async(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;
+    const bool async = async_ok && (force ? !strcmp(force, "async") : small);
+    const bool count = !async && count_ok && (force ? !strcmp(force, "count") : small);
     const bool coop_ok = ctx->adj16 != nullptr && V < 65535 &&
                          dfs_lds_bytes_coop(V) <= SDNR_MAX_LDS_PER_BLOCK;
     const bool coop = !count && coop_ok && (force ? !strcmp(force, "coop") : small);
-    if (count) {
+    if (async) {
+        int *err = ctx->d_err;
+        const size_t cl = dfs_lds_bytes_async(V, hops);
+        size_t cpc = SDNR_LDS_PER_CU / cl;
+        if (cpc > 8) cpc = 8;
+        if (cpc < 1) cpc = 1;
+        int cgrid = (int)((size_t)ctx->num_cus * cpc);
+        if (cgrid > nsrc) cgrid = nsrc;
+        const int nw = dfs_async_waves();
+        ctx->last_kernel = nw == 2 ? "dfs_async_kernel<2>" : nw == 3 ? "dfs_async_kernel<3>"
+                                                                    : "dfs_async_kernel<4>";
+#define SDNR_ASYNC(N_, H_)                                                                   \
+    do {                                                                                     \
+        auto k = dfs_async_kernel<N_, H_>;                                                   \
+        allow_full_lds(k);                                                                   \
+        hipLaunchKernelGGL(k, dim3(cgrid), dim3(N_ * 64), cl, ctx->stream, V, ctx->adj16,    \
+                           ctx->radj16, ctx->deg32, ctx->row_ptr, ctx->port, d_src, nsrc,    \
+                           d_parent, d_port, d_hops, err);                                   \
+    } while (0)
+        if (nw == 2) {
+            if (hops) SDNR_ASYNC(2, true); else SDNR_ASYNC(2, false);
+        } else if (nw == 3) {
+            if (hops) SDNR_ASYNC(3, true); else SDNR_ASYNC(3, false);
+        } else {
+            if (hops) SDNR_ASYNC(4, true); else SDNR_ASYNC(4, false);
+        }
+#undef SDNR_ASYNC
+    } else if (count) {
         const size_t cl = dfs_lds_bytes_count(V, hops);
         size_t cpc = SDNR_LDS_PER_CU / cl;
         if (cpc > 8) cpc = 8;

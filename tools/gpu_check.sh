@@ -7,8 +7,9 @@ timeout -k 10 600 python -m pytest tests/test_gpu_parity.py tests/test_topologyd
   --timeout 300 -k "dfs or dropin or Reference or scenarios or pairs or tables" > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 "$OUT/pytest_gpu.log"
 [ $rc -ne 0 ] && exit $rc
-for st in count4 count2 count6 coop; do
+for st in ${SWEEP:-async4 async3 async2 count2 coop}; do
   case $st in
+    async*) export SDNROUTE_DFS_STRATEGY=async SDNROUTE_DFS_ASYNC_WAVES=${st#async};;
     count*) export SDNROUTE_DFS_STRATEGY=count SDNROUTE_DFS_COUNT_WAVES=${st#count};;
     *) export SDNROUTE_DFS_STRATEGY=$st;;
   esac
