@@ -1109,10 +1109,18 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             int pub = 1, sp = 1, pu = -1, xpre = V;
+#ifdef SDNR_STAMPS
+            unsigned long long st_t0, st_t1, st_row = 0, st_cand = 0, st_false = 0, st_bp = 0,
+                                               st_miss = 0, st_skip = 0;
+            SDNR_STAMP(st_t0);
+#endif
             for (;;) {
                 uint64_t m = 0;
                 int e = V;
                 while (sp > 0) {
+#ifdef SDNR_STAMPS
+                    st_skip++;
+#endif
                     const int kk = sp < 64 ? sp : 64;
                     const int at = sp - 1 - lane;
                     e = stk[at < 0 ? 0 : at];
@@ -1127,10 +1135,21 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                 const int first = __ffsll((unsigned long long)m) - 1;
                 const int u = read_lane(e, first);
                 sp -= first + 1;
+#ifdef SDNR_STAMPS
+                unsigned long long ta, tb;
+                SDNR_STAMP(ta);
+                if (u != pu) st_miss++;
+#endif
                 const int x = (u == pu) ? xpre : (int)adj[(size_t)u * 64 + lane];
                 const uint32_t wv = vis[x >> 5];
                 const bool fresh = ((wv >> (x & 31)) & 1u) == 0u;
                 const uint64_t mm = __ballot(fresh);
+#ifdef SDNR_STAMPS
+                SDNR_STAMP(tb);
+                st_row += tb - ta;
+                st_cand++;
+                if (mm == 0) st_false++;
+#endif
                 if (mm == 0) continue;           // stale count: a leaf pop after all
                 const int c = __popcll(mm);
                 const int rank = lanes_below(mm);
@@ -1150,6 +1169,9 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                         if (lane == 0) atomicOr(err, 1);
                         break;
                     }
+#ifdef SDNR_STAMPS
+                    st_bp++;
+#endif
                     __builtin_amdgcn_s_sleep(1);
                 }
                 if (fresh) {
@@ -1166,6 +1188,17 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef SDNR_STAMPS
+            SDNR_STAMP(st_t1);
+            if (lane == 0) {
+                atomicAdd(&g_stamp[0], st_t1 - st_t0);   // search wave lifetime
+                atomicAdd(&g_stamp[1], st_row);          // row + gather cycles
+                atomicAdd(&g_stamp[2], st_cand);         // candidates popped
+                atomicAdd(&g_stamp[3], st_false);        // ... with no fresh child
+                atomicAdd(&g_stamp[4], st_bp);           // back-pressure sleeps
+                atomicAdd(&g_stamp[5], st_skip * 1000000ull + st_miss);   // skips, prefetch misses
+            }
+#endif
         } else {
             // ------------------------------------------------ the decrements
             int j = w - 1;                       // next child index of this worker
@@ -1367,7 +1400,7 @@ static int dfs_async_waves()
 {
     if (const char *f = getenv("SDNROUTE_DFS_ASYNC_WAVES")) {
         const int k = atoi(f);
-        if (k == 2 || k == 3 || k == 4) return k;
+        if (k >= 2 && k <= 6) return k;
     }
     return 4;
 }
@@ -1458,8 +1491,10 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         int cgrid = (int)((size_t)ctx->num_cus * cpc);
         if (cgrid > nsrc) cgrid = nsrc;
         const int nw = dfs_async_waves();
-        ctx->last_kernel = nw == 2 ? "dfs_async_kernel<2>" : nw == 3 ? "dfs_async_kernel<3>"
-                                                                    : "dfs_async_kernel<4>";
+        static const char *names[] = {"", "", "dfs_async_kernel<2>", "dfs_async_kernel<3>",
+                                      "dfs_async_kernel<4>", "dfs_async_kernel<5>",
+                                      "dfs_async_kernel<6>"};
+        ctx->last_kernel = names[nw];
 #define SDNR_ASYNC(N_, H_)                                                                   \
     do {                                                                                     \
         auto k = dfs_async_kernel<N_, H_>;                                                   \
@@ -1472,6 +1507,10 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
             if (hops) SDNR_ASYNC(2, true); else SDNR_ASYNC(2, false);
         } else if (nw == 3) {
             if (hops) SDNR_ASYNC(3, true); else SDNR_ASYNC(3, false);
+        } else if (nw == 5) {
+            if (hops) SDNR_ASYNC(5, true); else SDNR_ASYNC(5, false);
+        } else if (nw == 6) {
+            if (hops) SDNR_ASYNC(6, true); else SDNR_ASYNC(6, false);
         } else {
             if (hops) SDNR_ASYNC(4, true); else SDNR_ASYNC(4, false);
         }
