@@ -1076,7 +1076,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
     uint16_t *ring = reinterpret_cast<uint16_t *>(ps + V + (HOPS ? ((V + 1) >> 1) : 0));
     int *ctl = reinterpret_cast<int *>(ring + RING);   // [0] published [1] done [2+k] consumed
     const int lane = lane_id();
-    const int w = threadIdx.x >> 6;
+    const int w = uniform((int)(threadIdx.x >> 6));
 
     for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
         const int s = uniform(src[si]);
@@ -1108,7 +1108,11 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            int pub = 1, sp = 1, pu = -1, xpre = V;
+            // the search wave is the critical path: let it win issue arbitration
+            // against the decrement workers sharing its SIMD
+            __builtin_amdgcn_s_setprio(3);
+            int pub = 1, sp = 1, lo = 0;
+            int pu0 = -1, pu1 = -1, xpre0 = V, xpre1 = V;   // rows of the two largest children
 #ifdef SDNR_STAMPS
             unsigned long long st_t0, st_t1, st_row = 0, st_cand = 0, st_false = 0, st_bp = 0,
                                                st_miss = 0, st_skip = 0;
@@ -1138,9 +1142,10 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
 #ifdef SDNR_STAMPS
                 unsigned long long ta, tb;
                 SDNR_STAMP(ta);
-                if (u != pu) st_miss++;
+                if (u != pu0 && u != pu1) st_miss++;
 #endif
-                const int x = (u == pu) ? xpre : (int)adj[(size_t)u * 64 + lane];
+                const int x = (u == pu0) ? xpre0 : (u == pu1) ? xpre1
+                                                              : (int)adj[(size_t)u * 64 + lane];
                 const uint32_t wv = vis[x >> 5];
                 const bool fresh = ((wv >> (x & 31)) & 1u) == 0u;
                 const uint64_t mm = __ballot(fresh);
@@ -1153,16 +1158,21 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                 if (mm == 0) continue;           // stale count: a leaf pop after all
                 const int c = __popcll(mm);
                 const int rank = lanes_below(mm);
-                pu = read_lane(x, highest_lane(mm));
-                xpre = adj[(size_t)pu * 64 + lane];
+                // the next candidates are most likely the newest children
+                pu0 = read_lane(x, highest_lane(mm));
+                const uint64_t rest = mm & ~(1ull << highest_lane(mm));
+                pu1 = rest ? read_lane(x, highest_lane(rest)) : -1;
+                xpre0 = adj[(size_t)pu0 * 64 + lane];
+                xpre1 = adj[(size_t)(rest ? pu1 : V) * 64 + lane];
                 int du = 0;
                 if (HOPS) du = uniform((int)dep[u]);
-                // back-pressure: ring slots below every worker's progress are free
-                for (unsigned spin = 0;; ++spin) {
-                    int lo = 0x7FFFFFFF;
+                // back-pressure: ring slots below every worker's progress are
+                // free; the bound only needs refreshing when it would block
+                for (unsigned spin = 0; pub + c - lo > RING; ++spin) {
+                    lo = 0x7FFFFFFF;
 #pragma unroll
-                    for (int k = 0; k < S; ++k)
-                        lo = min(lo, __hip_atomic_load(&ctl[2 + k], __ATOMIC_RELAXED,
+                    for (int q = 0; q < S; ++q)
+                        lo = min(lo, __hip_atomic_load(&ctl[2 + q], __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_WORKGROUP));
                     if (pub + c - lo <= RING) break;
                     if (spin > kSpin) {
@@ -1188,6 +1198,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __builtin_amdgcn_s_setprio(0);
 #ifdef SDNR_STAMPS
             SDNR_STAMP(st_t1);
             if (lane == 0) {

@@ -1,0 +1,17 @@
+#!/bin/bash
+# One bench.py line per BASELINE config/mode (N=1).  Usage: bash tools/bench_all.sh OUTFILE
+OUT=${1:-gpurun_out/bench_all.jsonl}
+mkdir -p "$(dirname "$OUT")"; : > "$OUT"
+run() {  # fabric mode steps warmup extra...
+  timeout -k 10 ${TMO:-300} python bench.py --fabric "$1" --mode "$2" --steps "$3" --warmup "$4" "${@:5}" >> "$OUT" 2> "$OUT.$1.$2.err"
+  rc=$?; echo "$1 $2 rc=$rc"; case $rc in 124|134|137|139) exit $rc;; esac
+}
+run mock dfs 50 5
+run fat_tree:8 dfs 50 5
+run fat_tree:48 dfs 20 3
+run fat_tree:48 shortest 10 2 --no-cpu-baseline
+run dragonfly:16,8,8 dfs 10 2
+run dragonfly:16,8,8 shortest 5 1 --no-cpu-baseline
+TMO=600 run torus:32,32,32 dfs 2 1 --cpu-budget-s 8
+TMO=900 run jellyfish:100000,16,1 dfs 1 1 --cpu-budget-s 8
+exit 0
