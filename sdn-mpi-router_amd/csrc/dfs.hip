@@ -1061,7 +1061,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
     static_assert(NW >= 2, "wave 0 searches, the others decrement");
     constexpr int S = NW - 1;                    // workers
     constexpr int RING = 512;                    // children in flight (u16)
-    constexpr int G = 8;                         // rows in flight per worker
+    constexpr int G = NW <= 4 ? 16 : 8;          // rows in flight per worker
     constexpr unsigned kSpin = 1u << 22;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int VW = (V + 1 + 31) >> 5;
@@ -1108,9 +1108,6 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            // the search wave is the critical path: let it win issue arbitration
-            // against the decrement workers sharing its SIMD
-            __builtin_amdgcn_s_setprio(3);
             int pub = 1, sp = 1, lo = 0;
             int pu0 = -1, pu1 = -1, xpre0 = V, xpre1 = V;   // rows of the two largest children
 #ifdef SDNR_STAMPS
@@ -1198,7 +1195,6 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __builtin_amdgcn_s_setprio(0);
 #ifdef SDNR_STAMPS
             SDNR_STAMP(st_t1);
             if (lane == 0) {
