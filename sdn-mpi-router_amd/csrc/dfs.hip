@@ -1108,12 +1108,14 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            int pub = 1, sp = 1, lo = 0;
+            int pub = 1, pubd = 1, sp = 1, lo = 0;       // published / announced
             int pu0 = -1, pu1 = -1, xpre0 = V, xpre1 = V;   // rows of the two largest children
 #ifdef SDNR_STAMPS
             unsigned long long st_t0, st_t1, st_row = 0, st_cand = 0, st_false = 0, st_bp = 0,
-                                               st_miss = 0, st_skip = 0;
+                                               st_miss = 0, st_skip = 0, st_tc = 0, st_skipc = 0,
+                                               st_pushc = 0;
             SDNR_STAMP(st_t0);
+            st_tc = st_t0;
 #endif
             for (;;) {
                 uint64_t m = 0;
@@ -1132,6 +1134,14 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                     if (m) break;
                     sp -= kk;
                 }
+                // publish the previous push's children now: the skip's LDS
+                // reads have waited for those writes, so the release is free
+                if (pub != pubd) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (lane == 0) __hip_atomic_store(&ctl[0], pub, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                    pubd = pub;
+                }
                 if (!m) break;
                 const int first = __ffsll((unsigned long long)m) - 1;
                 const int u = read_lane(e, first);
@@ -1139,6 +1149,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
 #ifdef SDNR_STAMPS
                 unsigned long long ta, tb;
                 SDNR_STAMP(ta);
+                st_skipc += ta - st_tc;
                 if (u != pu0 && u != pu1) st_miss++;
 #endif
                 const int x = (u == pu0) ? xpre0 : (u == pu1) ? xpre1
@@ -1151,6 +1162,9 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                 st_row += tb - ta;
                 st_cand++;
                 if (mm == 0) st_false++;
+#endif
+#ifdef SDNR_STAMPS
+                if (mm == 0) st_tc = tb;
 #endif
                 if (mm == 0) continue;           // stale count: a leaf pop after all
                 const int c = __popcll(mm);
@@ -1190,8 +1204,10 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                 }
                 pub += c;
                 sp += c;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                if (lane == 0) __hip_atomic_store(&ctl[0], pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef SDNR_STAMPS
+                SDNR_STAMP(st_tc);
+                st_pushc += st_tc - tb;
+#endif
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1204,6 +1220,8 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                 atomicAdd(&g_stamp[3], st_false);        // ... with no fresh child
                 atomicAdd(&g_stamp[4], st_bp);           // back-pressure sleeps
                 atomicAdd(&g_stamp[5], st_skip * 1000000ull + st_miss);   // skips, prefetch misses
+                atomicAdd(&g_stamp[6], st_skipc);        // skip cycles
+                atomicAdd(&g_stamp[7], st_pushc);        // push+publish cycles
             }
 #endif
         } else {
@@ -1394,7 +1412,7 @@ static int dfs_coop_kw()
 #ifdef SDNR_STAMPS
 extern "C" int sdnr_debug_stamps(unsigned long long *out6)
 {
-    if (hipMemcpyFromSymbol(out6, HIP_SYMBOL(g_stamp), 6 * sizeof(unsigned long long)) !=
+    if (hipMemcpyFromSymbol(out6, HIP_SYMBOL(g_stamp), 8 * sizeof(unsigned long long)) !=
         hipSuccess)
         return -5;
     unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};

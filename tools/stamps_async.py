@@ -28,8 +28,8 @@ dev = torch.device("cuda", 0)
 ts = torch.from_numpy(srcs).to(dev)
 p = torch.empty((len(srcs), csr.V), dtype=torch.int32, device=dev)
 t = torch.empty_like(p)
-buf = (ctypes.c_ulonglong * 6)()
-for nw in (2, 3, 4, 5, 6):
+buf = (ctypes.c_ulonglong * 8)()
+for nw in (3, 4, 5):
     os.environ["SDNROUTE_DFS_ASYNC_WAVES"] = str(nw)
     for rep in range(2):
         L.sdnr_debug_stamps(buf)
@@ -40,6 +40,8 @@ for nw in (2, 3, 4, 5, 6):
     S = len(srcs)
     cand = buf[2] / S
     print("%s %.3f ms | per source: life %.0fk cyc, candidates %.1f (false %.1f), "
-          "row+gather %.0f cyc/cand, bp sleeps %.1f, skip steps %.1f, prefetch misses %.1f" % (
+          "row+gather %.0f cyc/cand, skip %.0f cyc/cand, push %.0f cyc/push, bp sleeps %.1f, "
+          "skip steps %.1f, prefetch misses %.1f" % (
               ctx.last_kernel(), ms, buf[0] / S / 1e3, cand, buf[3] / S, buf[1] / max(buf[2], 1),
+              buf[6] / max(buf[2], 1), buf[7] / max(buf[2] - buf[3], 1),
               buf[4] / S, (buf[5] // 1000000) / S, (buf[5] % 1000000) / S))
