@@ -20,6 +20,8 @@ from sdnmpi_amd import topologies as T  # noqa: E402
 fab = T.by_name(sys.argv[1] if len(sys.argv) > 1 else "fat_tree:48")
 csr = fab.csr()
 srcs = np.unique(fab.host_table()[0]).astype(np.int32)
+if len(sys.argv) > 2:                       # subset: fewer workgroups per CU
+    srcs = srcs[:: max(1, len(srcs) // int(sys.argv[2]))][: int(sys.argv[2])]
 L = _native.library()
 L.sdnr_debug_stamps.argtypes = [ctypes.c_void_p]
 ctx = _native.Context(0)
