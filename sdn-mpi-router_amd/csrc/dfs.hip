@@ -1050,6 +1050,12 @@ __global__ __launch_bounds__(64) void dfs_global_packed_kernel(
 // Every spin is bounded; the bound only trips on a bug, and then sets the
 // error word instead of hanging the GPU.
 // ---------------------------------------------------------------------------
+// LDS bank swizzle for per-vertex arrays indexed by neighbour ids: rows of
+// structured fabrics hold strided ids (a fat-tree core's neighbours are 24
+// apart: 8-way bank conflicts); x ^ ((x >> 3) & 31) is a bijection inside
+// every 256-entry block and spreads those rows over all 32 banks.
+__device__ __forceinline__ int swz(int x) { return x ^ ((x >> 3) & 31); }
+
 template <int NW, bool HOPS>
 __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
     int V, const uint16_t *__restrict__ adj, const uint16_t *__restrict__ radj,
@@ -1066,14 +1072,15 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int VW = (V + 1 + 31) >> 5;
     const int VWp = (VW + 3) & ~3;
-    const int CWp = (V + 1 + 3) & ~3;
+    const int CWp = (V + 1 + 255) & ~255;        // swizzled: whole 256-blocks
     const int SWp = (((V + 1) >> 1) + 3) & ~3;
+    const int PWp = (V + 255) & ~255;
     uint32_t *vis = lds;
-    uint32_t *cnt = vis + VWp;
+    uint32_t *cnt = vis + VWp;                   // cnt[swz(v)]
     uint16_t *stk = reinterpret_cast<uint16_t *>(cnt + CWp);
-    uint32_t *ps = cnt + CWp + SWp;
-    uint16_t *dep = reinterpret_cast<uint16_t *>(ps + V);
-    uint16_t *ring = reinterpret_cast<uint16_t *>(ps + V + (HOPS ? ((V + 1) >> 1) : 0));
+    uint32_t *ps = cnt + CWp + SWp;              // ps[swz(v)]
+    uint16_t *dep = reinterpret_cast<uint16_t *>(ps + PWp);   // dep[v]
+    uint16_t *ring = reinterpret_cast<uint16_t *>(ps + PWp + (HOPS ? ((V + 1) >> 1) : 0));
     int *ctl = reinterpret_cast<int *>(ring + RING);   // [0] published [1] done [2+k] consumed
     const int lane = lane_id();
     const int w = uniform((int)(threadIdx.x >> 6));
@@ -1092,7 +1099,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             continue;
         }
         for (int i = threadIdx.x; i < VW; i += blockDim.x) vis[i] = 0u;
-        for (int i = threadIdx.x; i <= V; i += blockDim.x) cnt[i] = deg[i];
+        for (int i = threadIdx.x; i <= V; i += blockDim.x) cnt[swz(i)] = deg[i];
         if (threadIdx.x < 2 + S) ctl[threadIdx.x] = 0;
         __syncthreads();
 
@@ -1101,7 +1108,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             if (lane == 0) {
                 vis[s >> 5] |= 1u << (s & 31);
                 vis[V >> 5] |= 1u << (V & 31);
-                ps[s] = (uint32_t)s;
+                ps[swz(s)] = (uint32_t)s;
                 if (HOPS) dep[s] = 0;
                 stk[0] = (uint16_t)s;
                 ring[0] = (uint16_t)s;           // s's in-neighbours lose one
@@ -1128,7 +1135,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                     const int at = sp - 1 - lane;
                     e = stk[at < 0 ? 0 : at];
                     e = lane < kk ? e : V;
-                    const uint32_t c = __hip_atomic_load(&cnt[e], __ATOMIC_RELAXED,
+                    const uint32_t c = __hip_atomic_load(&cnt[swz(e)], __ATOMIC_RELAXED,
                                                          __HIP_MEMORY_SCOPE_WORKGROUP);
                     m = __ballot(c != 0u);
                     if (m) break;
@@ -1197,7 +1204,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                 }
                 if (fresh) {
                     atomicOr(&vis[x >> 5], 1u << (x & 31));
-                    ps[x] = (uint32_t)u | ((uint32_t)lane << 16);
+                    ps[swz(x)] = (uint32_t)u | ((uint32_t)lane << 16);
                     if (HOPS) dep[x] = (uint16_t)(du + 1);
                     stk[sp + rank] = (uint16_t)x;
                     ring[(pub + rank) & (RING - 1)] = (uint16_t)x;
@@ -1248,7 +1255,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                 for (int g = 0; g < G; ++g) r[g] = radj[(size_t)read_lane(mine, g) * 64 + lane];
 #pragma unroll
                 for (int g = 0; g < G; ++g)
-                    if (g < n && r[g] != V) atomicSub(&cnt[r[g]], 1u);
+                    if (g < n && r[g] != V) atomicSub(&cnt[swz(r[g])], 1u);
                 j += n * S;
                 if (lane == 0) __hip_atomic_store(&ctl[2 + w - 1], j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
@@ -1258,7 +1265,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
         for (int v = threadIdx.x; v < V; v += blockDim.x) {
             int p = -1, pt = -1, h = -1;
             if ((vis[v >> 5] >> (v & 31)) & 1u) {
-                const uint32_t xx = ps[v];
+                const uint32_t xx = ps[swz(v)];
                 p = (int)(xx & 0xFFFFu);
                 if (v == s) {
                     h = 0;
@@ -1363,9 +1370,10 @@ static size_t dfs_lds_bytes_count(int V, bool hops)
 static size_t dfs_lds_bytes_async(int V, bool hops)
 {
     const size_t VWp = (size_t)((((V + 1 + 31) >> 5) + 3) & ~3);
-    const size_t CWp = (size_t)((V + 1 + 3) & ~3);
+    const size_t CWp = (size_t)((V + 1 + 255) & ~255);
     const size_t SWp = (size_t)((((V + 1) >> 1) + 3) & ~3);
-    return align16(4 * (VWp + CWp + SWp) + 4 * (size_t)V +
+    const size_t PWp = (size_t)((V + 255) & ~255);
+    return align16(4 * (VWp + CWp + SWp) + 4 * PWp +
                    (hops ? 4 * (size_t)((V + 1) >> 1) : 0) + 2 * 512 + 4 * 16);
 }
 
