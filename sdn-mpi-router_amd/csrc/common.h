@@ -32,6 +32,13 @@ __device__ __forceinline__ int read_lane(int x, int lane) {
 
 __device__ __forceinline__ int highest_lane(uint64_t m) { return 63 - __clzll(m); }
 
+// LDS bank swizzle for per-vertex u32 arrays indexed by neighbour ids: rows of
+// structured fabrics hold strided ids (a fat-tree core's neighbours are 24
+// apart: 8-way bank conflicts); x ^ ((x >> 3) & 31) is a bijection inside
+// every 256-entry block and spreads those rows over all 32 banks.  Arrays
+// indexed this way are sized in whole 256-entry blocks.
+__device__ __forceinline__ int lds_swz(int x) { return x ^ ((x >> 3) & 31); }
+
 // ------------------------------------------------------------------ host --
 
 struct sdnr_ctx {

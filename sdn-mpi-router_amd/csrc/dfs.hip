@@ -728,7 +728,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_coop_kernel(
 #ifdef SDNR_STAMPS
 // diagnostic build only: cycles per phase of the counted-pop loop, summed
 // over every source by wave 0 of each workgroup (never in the real kernel)
-__device__ unsigned long long g_stamp[8];
+__device__ unsigned long long g_stamp[16];
 #define SDNR_STAMP(t) \
     do { __builtin_amdgcn_sched_barrier(0); \
          asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory"); \
@@ -1050,21 +1050,18 @@ __global__ __launch_bounds__(64) void dfs_global_packed_kernel(
 // Every spin is bounded; the bound only trips on a bug, and then sets the
 // error word instead of hanging the GPU.
 // ---------------------------------------------------------------------------
-// LDS bank swizzle for per-vertex arrays indexed by neighbour ids: rows of
-// structured fabrics hold strided ids (a fat-tree core's neighbours are 24
-// apart: 8-way bank conflicts); x ^ ((x >> 3) & 31) is a bijection inside
-// every 256-entry block and spreads those rows over all 32 banks.
-__device__ __forceinline__ int swz(int x) { return x ^ ((x >> 3) & 31); }
+__device__ __forceinline__ int swz(int x) { return lds_swz(x); }   // common.h
 
 template <int NW, bool HOPS>
 __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
     int V, const uint16_t *__restrict__ adj, const uint16_t *__restrict__ radj,
     const uint32_t *__restrict__ deg, const int32_t *__restrict__ row_ptr,
-    const int32_t *__restrict__ port, const int32_t *__restrict__ src, int nsrc,
-    int32_t *__restrict__ out_parent, int32_t *__restrict__ out_port,
-    int32_t *__restrict__ out_hops, int *__restrict__ err)
+    const int32_t *__restrict__ port, int W, const int32_t *__restrict__ ell_port,
+    const int32_t *__restrict__ src, int nsrc, int32_t *__restrict__ out_parent,
+    int32_t *__restrict__ out_port, int32_t *__restrict__ out_hops, int *__restrict__ err)
 {
     static_assert(NW >= 2, "wave 0 searches, the others decrement");
+    constexpr int U = 4;                         // init / flush vertices per thread per step
     constexpr int S = NW - 1;                    // workers
     constexpr int RING = 512;                    // children in flight (u16)
     constexpr int G = NW <= 4 ? 16 : 8;          // rows in flight per worker
@@ -1084,6 +1081,10 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
     int *ctl = reinterpret_cast<int *>(ring + RING);   // [0] published [1] done [2+k] consumed
     const int lane = lane_id();
     const int w = uniform((int)(threadIdx.x >> 6));
+#ifdef SDNR_STAMPS
+    unsigned long long kstart;
+    SDNR_STAMP(kstart);
+#endif
 
     for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
         const int s = uniform(src[si]);
@@ -1098,10 +1099,31 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             }
             continue;
         }
+#ifdef SDNR_STAMPS
+        unsigned long long ph0, ph1, ph2, ph3;
+        SDNR_STAMP(ph0);
+#endif
         for (int i = threadIdx.x; i < VW; i += blockDim.x) vis[i] = 0u;
-        for (int i = threadIdx.x; i <= V; i += blockDim.x) cnt[swz(i)] = deg[i];
+        // counts start at the out-degrees: U independent loads per thread in
+        // flight before the LDS stores
+        for (int i0 = threadIdx.x; i0 <= V; i0 += U * blockDim.x) {
+            uint32_t dg[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int i = i0 + k * (int)blockDim.x;
+                dg[k] = deg[i <= V ? i : V];
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int i = i0 + k * (int)blockDim.x;
+                if (i <= V) cnt[swz(i)] = dg[k];
+            }
+        }
         if (threadIdx.x < 2 + S) ctl[threadIdx.x] = 0;
         __syncthreads();
+#ifdef SDNR_STAMPS
+        SDNR_STAMP(ph1);
+#endif
 
         if (w == 0) {
             // ------------------------------------------------ the search
@@ -1261,25 +1283,59 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             }
         }
         __syncthreads();
+#ifdef SDNR_STAMPS
+        SDNR_STAMP(ph2);
+#endif
 
-        for (int v = threadIdx.x; v < V; v += blockDim.x) {
-            int p = -1, pt = -1, h = -1;
-            if ((vis[v >> 5] >> (v & 31)) & 1u) {
-                const uint32_t xx = ps[swz(v)];
-                p = (int)(xx & 0xFFFFu);
-                if (v == s) {
-                    h = 0;
-                } else {
-                    pt = port[row_ptr[p] + (int)(xx >> 16)];
-                    h = HOPS ? (int)dep[v] : 0;
+        // tables: U vertices per thread, their port loads (one ELL load, or
+        // row_ptr + port) all in flight before the stores
+        for (int v0 = threadIdx.x; v0 < V; v0 += U * blockDim.x) {
+            int p[U], sl[U], pt[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int v = v0 + k * (int)blockDim.x;
+                p[k] = -1;
+                sl[k] = -1;
+                if (v < V && ((vis[v >> 5] >> (v & 31)) & 1u)) {
+                    const uint32_t xx = ps[swz(v)];
+                    p[k] = (int)(xx & 0xFFFFu);
+                    if (v != s) sl[k] = (int)(xx >> 16);
                 }
             }
-            prow[v] = p;
-            trow[v] = pt;
-            if (HOPS) hrow[v] = h;
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                pt[k] = -1;
+                if (sl[k] >= 0)
+                    pt[k] = W > 0 ? ell_port[(size_t)p[k] * W + sl[k]] : port[row_ptr[p[k]] + sl[k]];
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int v = v0 + k * (int)blockDim.x;
+                if (v < V) {
+                    prow[v] = p[k];
+                    trow[v] = pt[k];
+                    if (HOPS) hrow[v] = p[k] < 0 ? -1 : (v == s ? 0 : (int)dep[v]);
+                }
+            }
         }
         __syncthreads();
+#ifdef SDNR_STAMPS
+        SDNR_STAMP(ph3);
+        if (threadIdx.x == 0) {
+            atomicAdd(&g_stamp[8], ph1 - ph0);       // init
+            atomicAdd(&g_stamp[9], ph2 - ph1);       // search + worker tail
+            atomicAdd(&g_stamp[10], ph3 - ph2);      // flush
+        }
+#endif
     }
+#ifdef SDNR_STAMPS
+    if (threadIdx.x == 0) {                      // span of the launch: last end, first start
+        unsigned long long t;
+        SDNR_STAMP(t);
+        atomicMax(&g_stamp[11], t);
+        atomicMax(&g_stamp[12], ~kstart);
+    }
+#endif
 }
 
 template <typename Kern>
@@ -1418,12 +1474,12 @@ static int dfs_coop_kw()
 }
 
 #ifdef SDNR_STAMPS
-extern "C" int sdnr_debug_stamps(unsigned long long *out6)
+extern "C" int sdnr_debug_stamps(unsigned long long *out16)
 {
-    if (hipMemcpyFromSymbol(out6, HIP_SYMBOL(g_stamp), 8 * sizeof(unsigned long long)) !=
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamp), 16 * sizeof(unsigned long long)) !=
         hipSuccess)
         return -5;
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long z[16] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof z) == hipSuccess ? 0 : -5;
 }
 #endif
@@ -1533,8 +1589,8 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         auto k = dfs_async_kernel<N_, H_>;                                                   \
         allow_full_lds(k);                                                                   \
         hipLaunchKernelGGL(k, dim3(cgrid), dim3(N_ * 64), cl, ctx->stream, V, ctx->adj16,    \
-                           ctx->radj16, ctx->deg32, ctx->row_ptr, ctx->port, d_src, nsrc,    \
-                           d_parent, d_port, d_hops, err);                                   \
+                           ctx->radj16, ctx->deg32, ctx->row_ptr, ctx->port, ctx->W,         \
+                           ctx->ell_port, d_src, nsrc, d_parent, d_port, d_hops, err);       \
     } while (0)
         if (nw == 2) {
             if (hops) SDNR_ASYNC(2, true); else SDNR_ASYNC(2, false);

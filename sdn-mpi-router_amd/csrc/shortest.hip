@@ -18,6 +18,9 @@
 //  * nexthop: per (destination, vertex) the first (= smallest dense id =
 //    smallest dpid) out-neighbour one hop closer; the destination's dist row
 //    is staged in LDS, one thread per vertex scans its sorted row.
+#include <stdlib.h>
+#include <string.h>
+
 #include "common.h"
 
 namespace {
@@ -153,7 +156,226 @@ __global__ __launch_bounds__(256) void nexthop_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Per-destination BFS with fused next-hop extraction (V < 65534, in- and
+// out-degree <= 64 -- the k=48 fat-tree and dragonfly shapes).
+//
+// msbfs packs 64 destinations per mask word, which leaves ndst/64 workgroups
+// (18 for the 1,152 k=48 edge switches), each sweeping every edge per level.
+// Here one workgroup owns one destination d and loads each vertex's row once:
+// dist(., d) lives in LDS (u32, bank-swizzled), the frontier of level L is a
+// contiguous range of an LDS queue (every vertex enters once), and expanding
+// y loads y's in-row (u16, stride 64: one 128-byte line), gathers the
+// in-neighbours' levels, claims the unseen ones for level L+1 with
+// ds_cmpswap and appends them with one queue-tail atomic per batch of rows
+// (ballot + mbcnt order the slots).  On a symmetric graph the same row is
+// y's out-row and its level-(L-1) entries are final, so y's next hop -- the
+// smallest out-neighbour one hop closer, the reference's lexicographic
+// tie-break -- is the lowest lane of a second ballot over the row already in
+// registers; asymmetric graphs run one pass over the out-rows afterwards.
+// The tables are written once per destination, coalesced.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kUnseen = 0xFFFFu;           // == SDNR_DIST_INF
+constexpr uint32_t kSentLevel = 0xFFFEu;        // level of the padding vertex V
+
+// LDS words of bfs_dest_kernel: lvl u32 [256-blocks], queue u16, nh u16,
+// nh slot u8, 4 control words
+__host__ __device__ inline int bfs_dest_qwords(int V) { return ((V + 1) / 2 + 3) & ~3; }
+__host__ __device__ inline int bfs_dest_words(int V)
+{
+    return ((V + 1 + 255) & ~255) + 2 * bfs_dest_qwords(V) + (((V + 3) / 4 + 3) & ~3) + 4;
+}
+
+template <int NW, int G, bool SYM>
+__global__ __launch_bounds__(NW * 64) void bfs_dest_kernel(
+    int V, int W, const uint16_t *__restrict__ adj, const uint16_t *__restrict__ radj,
+    const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ port,
+    const int32_t *__restrict__ ell_port, const int32_t *__restrict__ dst, int ndst,
+    uint16_t *__restrict__ out_dist, int32_t *__restrict__ out_nh,
+    int32_t *__restrict__ out_nh_port)
+{
+    constexpr int U = 4;                         // flush vertices per thread per step
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int DWp = (V + 1 + 255) & ~255;
+    const int QWp = bfs_dest_qwords(V);
+    uint32_t *lvl = lds;                                              // lvl[swz(v)]
+    uint16_t *q = reinterpret_cast<uint16_t *>(lvl + DWp);            // BFS order
+    uint16_t *nhv = reinterpret_cast<uint16_t *>(lvl + DWp + QWp);    // next hop
+    uint8_t *nhs = reinterpret_cast<uint8_t *>(lvl + DWp + 2 * QWp);  // its row slot
+    int *ctl = reinterpret_cast<int *>(lds + bfs_dest_words(V) - 4);  // [0] queue tail
+    const uint16_t *inrow = SYM ? adj : radj;
+    const int lane = lane_id();
+    const int w = uniform((int)(threadIdx.x >> 6));
+    const bool want_nh = out_nh != nullptr;
+
+    for (int di = blockIdx.x; di < ndst; di += gridDim.x) {
+        const int d = uniform(dst[di]);
+        uint16_t *drow = out_dist + (size_t)di * V;
+        int32_t *hrow = want_nh ? out_nh + (size_t)di * V : nullptr;
+        int32_t *prow = want_nh ? out_nh_port + (size_t)di * V : nullptr;
+        if (d < 0 || d >= V) {                   // unknown destination: empty row
+            for (int v = threadIdx.x; v < V; v += blockDim.x) {
+                drow[v] = (uint16_t)kUnseen;
+                if (want_nh) {
+                    hrow[v] = -1;
+                    prow[v] = -1;
+                }
+            }
+            continue;
+        }
+        for (int i = threadIdx.x; i <= V; i += blockDim.x)
+            lvl[lds_swz(i)] = i == d ? 0u : (i == V ? kSentLevel : kUnseen);
+        if (threadIdx.x == 0) {
+            q[0] = (uint16_t)d;
+            ctl[0] = 1;
+        }
+        __syncthreads();
+
+        int lo = 0, hi = 1;
+        for (int L = 0; lo < hi; ++L) {
+            // ---- expand level L = q[lo, hi): G rows per wave in flight
+            for (int base = lo + w * G; base < hi; base += NW * G) {
+                const int n = min(G, hi - base);
+                const int mine = lane < n ? (int)q[base + lane] : V;   // past n: sentinel row
+                int r[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    r[g] = inrow[(size_t)read_lane(mine, g) * 64 + lane];
+                uint32_t lv[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) lv[g] = lvl[lds_swz(r[g])];
+                uint32_t old[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    old[g] = kSentLevel;
+                    if (lv[g] == kUnseen)
+                        old[g] = atomicCAS(&lvl[lds_swz(r[g])], kUnseen, (uint32_t)(L + 1));
+                }
+                uint64_t fm[G];
+                int tot = 0;
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    fm[g] = __ballot(old[g] == kUnseen);
+                    tot += __popcll(fm[g]);
+                }
+                if (tot) {
+                    int at = 0;
+                    if (lane == 0) at = atomicAdd(&ctl[0], tot);
+                    at = uniform(at);
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        if ((fm[g] >> lane) & 1ull) q[at + lanes_below(fm[g])] = (uint16_t)r[g];
+                        at += __popcll(fm[g]);
+                    }
+                }
+                if (SYM && L > 0) {
+                    // next hop of each expanded y: lowest slot one level closer
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        if (g < n) {
+                            const uint64_t m = __ballot(lv[g] == (uint32_t)(L - 1));
+                            if (m) {
+                                // readlane with every lane active: an operand the
+                                // compiler sinks into a lane-0-only block would
+                                // leave the other lanes' values unwritten
+                                const int sl = __ffsll((unsigned long long)m) - 1;
+                                const int y = read_lane(mine, g);
+                                const int nb = read_lane(r[g], sl);
+                                if (lane == 0) {
+                                    nhv[y] = (uint16_t)nb;
+                                    nhs[y] = (uint8_t)sl;
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            __syncthreads();                     // level L+1 complete
+            lo = hi;
+            hi = ctl[0];
+            __syncthreads();                     // every wave has read the tail
+        }
+
+        if (!SYM && want_nh) {
+            // next hop over the out-rows: lowest slot whose level is one less
+            for (int base = w * G; base < V; base += NW * G) {
+                int r[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const int v = base + g < V ? base + g : V;
+                    r[g] = adj[(size_t)v * 64 + lane];
+                }
+                uint32_t lv[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) lv[g] = lvl[lds_swz(r[g])];
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const int v = base + g;
+                    if (v < V) {
+                        const uint32_t lx = lvl[lds_swz(v)];
+                        if (lx != kUnseen && lx != 0u) {
+                            const uint64_t m = __ballot(lv[g] + 1u == lx);
+                            if (m) {
+                                const int sl = __ffsll((unsigned long long)m) - 1;
+                                const int nb = read_lane(r[g], sl);
+                                if (lane == 0) {
+                                    nhv[v] = (uint16_t)nb;
+                                    nhs[v] = (uint8_t)sl;
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+        }
+
+        // ---- tables: U vertices per thread, port loads in flight together
+        for (int v0 = threadIdx.x; v0 < V; v0 += U * blockDim.x) {
+            uint32_t lx[U];
+            int h[U], sl[U], pt[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int v = v0 + k * (int)blockDim.x;
+                lx[k] = v < V ? lvl[lds_swz(v)] : kUnseen;
+                h[k] = -1;
+                sl[k] = -1;
+                if (want_nh && lx[k] != kUnseen && lx[k] != 0u) {
+                    h[k] = nhv[v];
+                    sl[k] = nhs[v];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int v = v0 + k * (int)blockDim.x;
+                pt[k] = -1;
+                if (sl[k] >= 0)
+                    pt[k] = W > 0 ? ell_port[(size_t)v * W + sl[k]] : port[row_ptr[v] + sl[k]];
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int v = v0 + k * (int)blockDim.x;
+                if (v < V) {
+                    drow[v] = (uint16_t)lx[k];
+                    if (want_nh) {
+                        hrow[v] = h[k];
+                        prow[v] = pt[k];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
+
+// SDNROUTE_SP_STRATEGY=msbfs|dest forces the shortest-mode kernel (tests)
+static const char *sp_strategy()
+{
+    const char *f = getenv("SDNROUTE_SP_STRATEGY");
+    return f ? f : "";
+}
 
 int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
                          uint16_t *d_dist, int32_t *d_nh, int32_t *d_nh_port)
@@ -162,6 +384,45 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
     if (ndst == 0 || V == 0) return SDNR_OK;
     const int nbatch = (ndst + 63) / 64;
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
+    const size_t dlds = (size_t)bfs_dest_words(V) * 4;
+    const bool dest_ok = ctx->adj16 != nullptr && ctx->radj16 != nullptr && V < 65534 &&
+                         dlds <= 64 * 1024;
+    const char *force = sp_strategy();
+    if (dest_ok && strcmp(force, "msbfs") != 0) {
+        const bool sym = ctx->radj16 == ctx->adj16;
+        size_t bpc = SDNR_LDS_PER_CU / dlds;
+        if (bpc > 8) bpc = 8;
+        int grid = (int)((size_t)ctx->num_cus * bpc);
+        if (grid > ndst) grid = ndst;
+        // SDNROUTE_SP_VARIANT: 0 = 4 waves x 16 rows in flight (default),
+        // 1 = 4 x 8, 2 = 8 x 8 (tuning)
+        const char *vf = getenv("SDNROUTE_SP_VARIANT");
+        const int var = vf ? atoi(vf) : 0;
+        static const char *names[2][3] = {
+            {"bfs_dest_kernel<4,16,asym>", "bfs_dest_kernel<4,8,asym>", "bfs_dest_kernel<8,8,asym>"},
+            {"bfs_dest_kernel<4,16,sym>", "bfs_dest_kernel<4,8,sym>", "bfs_dest_kernel<8,8,sym>"}};
+        const int vi = (var == 1 || var == 2) ? var : 0;
+        ctx->last_kernel = names[sym ? 1 : 0][vi];
+#define SDNR_BFS_DEST(NW_, G_, S_)                                                           \
+    do {                                                                                     \
+        auto k = bfs_dest_kernel<NW_, G_, S_>;                                               \
+        sdnr_allow_lds(reinterpret_cast<const void *>(k), dlds);                             \
+        hipLaunchKernelGGL(k, dim3(grid), dim3(NW_ * 64), dlds, ctx->stream, V, ctx->W,      \
+                           ctx->adj16, ctx->radj16, ctx->row_ptr, ctx->port, ctx->ell_port,  \
+                           d_dst, ndst, d_dist, d_nh, d_nh_port);                            \
+    } while (0)
+        if (vi == 1) {
+            if (sym) SDNR_BFS_DEST(4, 8, true); else SDNR_BFS_DEST(4, 8, false);
+        } else if (vi == 2) {
+            if (sym) SDNR_BFS_DEST(8, 8, true); else SDNR_BFS_DEST(8, 8, false);
+        } else {
+            if (sym) SDNR_BFS_DEST(4, 16, true); else SDNR_BFS_DEST(4, 16, false);
+        }
+#undef SDNR_BFS_DEST
+        SDNR_HIP(hipGetLastError());
+        if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+        return SDNR_OK;
+    }
     SDNR_HIP(hipMemsetAsync(d_dist, 0xFF, (size_t)ndst * V * sizeof(uint16_t), ctx->stream));
     const size_t lds = (size_t)V * 3 * sizeof(uint64_t);
     ctx->last_kernel = lds <= 150 * 1024 ? "msbfs_lds_kernel+nexthop_kernel"

@@ -131,8 +131,11 @@ def test_dfs_fullsize_tree_properties(ctx):
             assert k < hi and csr.col[k] == v and csr.port[k] == t[s, v]
 
 
+@pytest.mark.parametrize("strategy", ["auto", "msbfs"])
 @pytest.mark.parametrize("name", G.SMALL)
-def test_shortest_small_all_destinations(ctx, name):
+def test_shortest_small_all_destinations(ctx, monkeypatch, name, strategy):
+    if strategy != "auto":
+        monkeypatch.setenv("SDNROUTE_SP_STRATEGY", strategy)
     fabric = G.Golden(name).fabric()
     csr = fabric.csr()
     dsts = np.arange(csr.V, dtype=np.int32)
@@ -165,12 +168,17 @@ def test_shortest_matches_reference_multiple(ctx, name):
             assert [int(csr.dpids[x]) for x in q] == [x for x, _ in w]
 
 
-def test_shortest_fullsize_fat_tree(ctx):
+@pytest.mark.parametrize("strategy", ["auto", "msbfs"])
+def test_shortest_fullsize_fat_tree(ctx, monkeypatch, strategy):
+    if strategy != "auto":
+        monkeypatch.setenv("SDNROUTE_SP_STRATEGY", strategy)
     fabric = T.fat_tree(48)
     csr = fabric.csr()
     dsts = np.unique(fabric.host_table()[0]).astype(np.int32)
     ctx.upload(csr)
     dist, nh, nhp = ctx.shortest_tables(dsts)
+    if strategy == "auto":
+        assert ctx.last_kernel().startswith("bfs_dest_kernel")
     do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
     np.testing.assert_array_equal(dist, do)
     np.testing.assert_array_equal(nh, nho)
@@ -196,6 +204,34 @@ def test_apsp_small(ctx, name):
     csr = G.Golden(name).fabric().csr()
     ctx.upload(csr)
     np.testing.assert_array_equal(ctx.apsp(), O.apsp(csr))
+
+
+def test_shortest_dest_kernel_dragonfly_all_destinations(ctx):
+    csr = T.dragonfly(16, 8, 8).csr()
+    dsts = np.arange(csr.V, dtype=np.int32)
+    ctx.upload(csr)
+    dist, nh, nhp = ctx.shortest_tables(dsts)
+    assert ctx.last_kernel().startswith("bfs_dest_kernel")
+    do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
+    np.testing.assert_array_equal(dist, do)
+    np.testing.assert_array_equal(nh, nho)
+    np.testing.assert_array_equal(nhp, nhpo)
+
+
+def test_shortest_unknown_destination_rows_device(ctx):
+    torch = pytest.importorskip("torch")
+    csr = T.fat_tree(4).csr()
+    ctx.upload(csr)
+    dev = torch.device("cuda", 0)
+    td = torch.tensor([-1, 3, csr.V + 5], dtype=torch.int32, device=dev)
+    dist = torch.zeros((3, csr.V), dtype=torch.int16, device=dev)
+    nh = torch.zeros((3, csr.V), dtype=torch.int32, device=dev)
+    nhp = torch.zeros_like(nh)
+    ctx.shortest_tables_device(td.data_ptr(), 3, dist.data_ptr(), nh.data_ptr(), nhp.data_ptr())
+    ctx.synchronize()
+    d = dist.cpu().numpy().view(np.uint16)
+    assert (d[0] == 0xFFFF).all() and (d[2] == 0xFFFF).all() and d[1, 3] == 0
+    assert (nh.cpu().numpy()[[0, 2]] == -1).all()
 
 
 def test_apsp_matches_msbfs_dragonfly(ctx):

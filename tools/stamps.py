@@ -31,7 +31,7 @@ dev = torch.device("cuda", 0)
 ts = torch.from_numpy(srcs).to(dev)
 p = torch.empty((len(srcs), csr.V), dtype=torch.int32, device=dev)
 t = torch.empty_like(p)
-buf = (ctypes.c_ulonglong * 6)()
+buf = (ctypes.c_ulonglong * 16)()
 for rep in range(3):
     L.sdnr_debug_stamps(buf)            # reset
     ctx.dfs_tables_device(ts.data_ptr(), len(srcs), p.data_ptr(), t.data_ptr(), timing=True)

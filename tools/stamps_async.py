@@ -30,7 +30,7 @@ dev = torch.device("cuda", 0)
 ts = torch.from_numpy(srcs).to(dev)
 p = torch.empty((len(srcs), csr.V), dtype=torch.int32, device=dev)
 t = torch.empty_like(p)
-buf = (ctypes.c_ulonglong * 8)()
+buf = (ctypes.c_ulonglong * 16)()
 for nw in (3, 4, 5):
     os.environ["SDNROUTE_DFS_ASYNC_WAVES"] = str(nw)
     for rep in range(2):
@@ -47,3 +47,7 @@ for nw in (3, 4, 5):
               ctx.last_kernel(), ms, buf[0] / S / 1e3, cand, buf[3] / S, buf[1] / max(buf[2], 1),
               buf[6] / max(buf[2], 1), buf[7] / max(buf[2] - buf[3], 1),
               buf[4] / S, (buf[5] // 1000000) / S, (buf[5] % 1000000) / S))
+    span = buf[11] - (~buf[12] & 0xFFFFFFFFFFFFFFFF)
+    print("    per source: init %.1fk cyc, search+worker tail %.1fk cyc, flush %.1fk cyc; "
+          "launch span %.1fk cyc" % (buf[8] / S / 1e3, buf[9] / S / 1e3, buf[10] / S / 1e3,
+                                     span / 1e3))
