@@ -63,7 +63,28 @@ def main(src, out):
                 100 * c.get("SQ_ACTIVE_INST_ANY", 0) / wc))
     open(out + "_summary.md", "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
+    return pmc
+
+
+def record_traffic(pmc, key, kernel_prefix, path):
+    """Store the corrected HBM bytes per dispatch of the dominant kernel in
+    profiles/traffic.json under `key` ("fabric/mode/N<n>"); bench.py reports
+    it as roofline.traffic."""
+    hits = [d for k, d in pmc.items() if kernel_prefix in k]
+    if not hits:
+        raise SystemExit("no PMC rows for kernel %r" % kernel_prefix)
+    c = hits[0]["counters"]
+    if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
+        raise SystemExit("FETCH_SIZE / WRITE_SIZE missing for %r" % kernel_prefix)
+    tb = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+    data = json.load(open(path)) if os.path.exists(path) else {}
+    data[key] = tb
+    json.dump(data, open(path, "w"), indent=1, sort_keys=True)
+    print("traffic %s = %.4g bytes per dispatch -> %s" % (key, tb, path))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    res = main(sys.argv[1], sys.argv[2])
+    if len(sys.argv) > 4:      # ... KEY KERNEL_PREFIX  -> profiles/traffic.json
+        record_traffic(res, sys.argv[3], sys.argv[4],
+                       os.path.join(os.path.dirname(sys.argv[2]) or ".", "traffic.json"))
