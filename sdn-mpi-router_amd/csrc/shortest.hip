@@ -83,24 +83,41 @@ __global__ __launch_bounds__(kBfsThreads) void msbfs_lds_kernel(
     }
 }
 
-// one BFS level for every batch; masks [nbatch][V] in global memory
+// one BFS level for every batch; masks [nbatch][V] in global memory.  A
+// vertex every destination of its batch has already reached is skipped (no
+// neighbour gather); ELL rows (W > 0) are read with W independent loads.
 __global__ __launch_bounds__(256) void msbfs_level_kernel(
-    int V, const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
-    int ndst, int lvl, const uint64_t *__restrict__ front,
-    uint64_t *__restrict__ next, uint64_t *__restrict__ vis,
-    uint16_t *__restrict__ dist, int *__restrict__ changed)
+    int V, int W, const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+    const int32_t *__restrict__ ell_col, int ndst, int lvl, const uint64_t *__restrict__ front,
+    uint64_t *__restrict__ next, uint64_t *__restrict__ vis, uint16_t *__restrict__ dist,
+    int *__restrict__ changed)
 {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int batch = blockIdx.y;
     if (x >= V) return;
     const size_t off = (size_t)batch * V;
+    const int nb = min(64, ndst - batch * 64);
+    const uint64_t all = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
+    const uint64_t vx = vis[off + x];
+    if ((vx & all) == all) {                  // nothing left to reach at x
+        next[off + x] = 0;
+        return;
+    }
     uint64_t acc = 0;
-    const int re = row_ptr[x + 1];
-    for (int e = row_ptr[x]; e < re; ++e) acc |= front[off + col[e]];
-    const uint64_t nw = acc & ~vis[off + x];
+    if (W > 0) {
+        const int32_t *r = ell_col + (size_t)x * W;
+        for (int j = 0; j < W; ++j) {
+            const int n = r[j];
+            if (n >= 0) acc |= front[off + n];
+        }
+    } else {
+        const int re = row_ptr[x + 1];
+        for (int e = row_ptr[x]; e < re; ++e) acc |= front[off + col[e]];
+    }
+    const uint64_t nw = acc & ~vx;
     next[off + x] = nw;
     if (nw) {
-        vis[off + x] |= nw;
+        vis[off + x] = vx | nw;
         write_levels(nw, batch * 64, ndst, V, x, (uint16_t)lvl, dist);
         *changed = 1;
     }
@@ -120,39 +137,57 @@ __global__ __launch_bounds__(256) void msbfs_seed_kernel(
     dist[(size_t)i * V + d] = 0;
 }
 
-// nh/nh_port for destination blockIdx.y, vertices in blockIdx.x's range
-__global__ __launch_bounds__(256) void nexthop_kernel(
-    int V, const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
-    const int32_t *__restrict__ port, const uint16_t *__restrict__ dist,
-    int32_t *__restrict__ nh, int32_t *__restrict__ nh_port, int stage)
+// nh/nh_port of whole destination rows, one 1024-thread workgroup per row:
+// the row's distances are staged in LDS once (V <= 32768) and every vertex
+// tests its W ELL neighbours with independent loads, keeping the first (=
+// smallest dpid) one hop closer.
+__global__ __launch_bounds__(1024) void nexthop_kernel(
+    int V, int W, int ndst, const int32_t *__restrict__ row_ptr,
+    const int32_t *__restrict__ col, const int32_t *__restrict__ port,
+    const int32_t *__restrict__ ell_col, const int32_t *__restrict__ ell_port,
+    const uint16_t *__restrict__ dist, int32_t *__restrict__ nh,
+    int32_t *__restrict__ nh_port, int stage)
 {
     extern __shared__ __attribute__((aligned(16))) uint16_t ldist[];
-    const size_t row = (size_t)blockIdx.y * V;
-    const uint16_t *drow = dist + row;
-    if (stage) {
-        for (int x = threadIdx.x; x < V; x += blockDim.x) ldist[x] = drow[x];
-        __syncthreads();
-        drow = ldist;
-    }
-    const int per = (V + gridDim.x - 1) / gridDim.x;
-    const int lo = blockIdx.x * per;
-    const int hi = min(V, lo + per);
-    for (int x = lo + threadIdx.x; x < hi; x += blockDim.x) {
-        const uint32_t dx = drow[x];
-        int best = -1, bport = -1;
-        if (dx != 0xFFFFu && dx != 0u) {
-            const int re = row_ptr[x + 1];
-            for (int e = row_ptr[x]; e < re; ++e) {
-                const int n = col[e];
-                if ((uint32_t)drow[n] + 1u == dx) {
-                    best = n;
-                    bport = port[e];
-                    break;
+    for (int rowi = blockIdx.x; rowi < ndst; rowi += gridDim.x) {
+        const size_t row = (size_t)rowi * V;
+        const uint16_t *drow = dist + row;
+        if (stage) {
+            __syncthreads();                     // previous row's readers are done
+            for (int x = threadIdx.x; x < V; x += blockDim.x) ldist[x] = drow[x];
+            __syncthreads();
+            drow = ldist;
+        }
+        for (int x = threadIdx.x; x < V; x += blockDim.x) {
+            const uint32_t dx = drow[x];
+            int best = -1, bport = -1;
+            if (dx != 0xFFFFu && dx != 0u) {
+                if (W > 0) {
+                    const int32_t *r = ell_col + (size_t)x * W;
+                    int bj = -1;
+                    for (int j = W - 1; j >= 0; --j) {   // no early exit: loads overlap
+                        const int n = r[j];
+                        if (n >= 0 && (uint32_t)drow[n] + 1u == dx) {
+                            best = n;
+                            bj = j;
+                        }
+                    }
+                    if (bj >= 0) bport = ell_port[(size_t)x * W + bj];
+                } else {
+                    const int re = row_ptr[x + 1];
+                    for (int e = row_ptr[x]; e < re; ++e) {
+                        const int n = col[e];
+                        if ((uint32_t)drow[n] + 1u == dx) {
+                            best = n;
+                            bport = port[e];
+                            break;
+                        }
+                    }
                 }
             }
+            nh[row + x] = best;
+            nh_port[row + x] = bport;
         }
-        nh[row + x] = best;
-        nh_port[row + x] = bport;
     }
 }
 
@@ -450,8 +485,8 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
         for (int lvl = 1; lvl < 0xFFFF && h_changed; ++lvl) {
             SDNR_HIP(hipMemsetAsync(changed, 0, sizeof(int), ctx->stream));
             hipLaunchKernelGGL(msbfs_level_kernel, dim3((V + 255) / 256, nbatch), dim3(256),
-                               0, ctx->stream, V, ctx->row_ptr, ctx->col, ndst, lvl,
-                               front, next, vis, d_dist, changed);
+                               0, ctx->stream, V, ctx->W, ctx->row_ptr, ctx->col, ctx->ell_col,
+                               ndst, lvl, front, next, vis, d_dist, changed);
             SDNR_HIP(hipGetLastError());
             SDNR_HIP(hipMemcpyAsync(&h_changed, changed, sizeof(int), hipMemcpyDeviceToHost,
                                     ctx->stream));
@@ -463,11 +498,13 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
     }
     if (d_nh && d_nh_port) {
         const int stage = (size_t)V * 2 <= 64 * 1024;
-        int gx = (V + 1023) / 1024;
-        if (gx < 1) gx = 1;
-        hipLaunchKernelGGL(nexthop_kernel, dim3(gx, ndst), dim3(256),
-                           stage ? (size_t)V * 2 : 0, ctx->stream, V, ctx->row_ptr,
-                           ctx->col, ctx->port, d_dist, d_nh, d_nh_port, stage);
+        int grid = ctx->num_cus * 8;
+        if (grid > ndst) grid = ndst;
+        auto k = nexthop_kernel;
+        if (stage) sdnr_allow_lds(reinterpret_cast<const void *>(k), (size_t)V * 2);
+        hipLaunchKernelGGL(k, dim3(grid), dim3(1024), stage ? (size_t)V * 2 : 0, ctx->stream, V,
+                           ctx->W, ndst, ctx->row_ptr, ctx->col, ctx->port, ctx->ell_col,
+                           ctx->ell_port, d_dist, d_nh, d_nh_port, stage);
         SDNR_HIP(hipGetLastError());
     }
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
