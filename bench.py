@@ -54,16 +54,20 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--fabric", default="fat_tree:48")
     ap.add_argument("--mode", choices=["dfs", "shortest"], default="dfs")
+    ap.add_argument("--layout", choices=["auto", "packed", "int32"], default="auto",
+                    help="dfs tables: packed u32 (parent | port << 16) when the fabric "
+                         "allows it (V <= 65535, 16-bit ports), else int32 parent + port")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0,
                     help="bound on the CPU baseline's work")
     return ap.parse_args()
 
 
-def algorithmic_bytes_per_source(V, E, mode):
+def algorithmic_bytes_per_source(V, E, mode, packed=False):
     if mode == "dfs":
-        # row_ptr + col (CSR read per source) + tree-edge port reads + parent/port writes
-        return 4 * (V + 1) + 4 * E + 4 * (V - 1) + 8 * V
+        # row_ptr + col (CSR read per source) + tree-edge port reads + table writes
+        # (parent + port: 8 B per vertex as int32, 4 B packed)
+        return 4 * (V + 1) + 4 * E + 4 * (V - 1) + (4 if packed else 8) * V
     # shortest: CSR read + dist (2 B) + nh/nh_port (8 B) writes per destination
     return 4 * (V + 1) + 4 * E + 10 * V
 
@@ -150,7 +154,14 @@ def main():
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     t_src = my.to(dev)
-    if args.mode == "dfs":
+    packed = args.mode == "dfs" and args.layout != "int32" and V <= 0xFFFF and \
+        csr.E > 0 and int(csr.port.min()) >= 0 and int(csr.port.max()) < 0xFFFF
+    if args.layout == "packed" and not packed:
+        raise SystemExit("--layout packed: fabric has V > 65535 or ports >= 0xFFFF")
+    if packed:
+        a = torch.empty((per, V), dtype=torch.int32, device=dev)     # parent | port << 16
+        b = c = None
+    elif args.mode == "dfs":
         a = torch.empty((per, V), dtype=torch.int32, device=dev)     # parent
         b = torch.empty((per, V), dtype=torch.int32, device=dev)     # port
         c = None
@@ -162,7 +173,9 @@ def main():
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        if args.mode == "dfs":
+        if packed:
+            ctx.dfs_tables_packed_device(t_src.data_ptr(), per, a.data_ptr())
+        elif args.mode == "dfs":
             ctx.dfs_tables_device(t_src.data_ptr(), per, a.data_ptr(), b.data_ptr())
         else:
             ctx.shortest_tables_device(t_src.data_ptr(), per, a.data_ptr(), b.data_ptr(),
@@ -198,13 +211,15 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     routes = float(H) * float(H)                 # every host pair, every step
     value = routes / (ms_per_step / 1e3)
-    bytes_launch = algorithmic_bytes_per_source(V, E, args.mode) * (hi - lo)
+    bytes_launch = algorithmic_bytes_per_source(V, E, args.mode, packed) * (hi - lo)
     achieved = bytes_launch / (kern_ms / 1e3) / 1e9
     traffic = None
+    layout = "packed" if packed else ("int32" if args.mode == "dfs" else "u16+int32")
     if os.path.exists(TRAFFIC_FILE):
         try:
             tf = json.load(open(TRAFFIC_FILE))
-            traffic = tf.get("%s/%s/N%d" % (args.fabric, args.mode, world))
+            traffic = tf.get("%s/%s%s/N%d" % (args.fabric, args.mode,
+                                               "-packed" if packed else "", world))
         except Exception:   # noqa: BLE001
             traffic = None
     out = {
@@ -225,7 +240,7 @@ def main():
                 args.fabric, args.mode,
                 "" if args.mode == "dfs" else "(multiple=True)[0] + dist"),
             "fabric": args.fabric, "V": V, "E": E, "hosts": H, "sources": S,
-            "host_pairs_per_step": int(routes),
+            "host_pairs_per_step": int(routes), "table_layout": layout,
             "parallelism": "sources sharded over %d GPU(s)%s" % (
                 world, " + RCCL all-gather" if world > 1 else ""),
         },

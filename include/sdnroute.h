@@ -46,6 +46,7 @@ extern "C" {
 
 #define SDNR_UNREACHED (-1)
 #define SDNR_DIST_INF  0xFFFFu
+#define SDNR_TREE_NONE 0xFFFFFFFFu
 
 typedef struct sdnr_ctx sdnr_ctx;
 
@@ -98,6 +99,17 @@ int sdnr_graph_info(const sdnr_ctx *ctx, int32_t *V, int32_t *E,
 int sdnr_dfs_tables(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc,
                     int32_t *parent, int32_t *port, int32_t *hops,
                     uint32_t flags);
+
+/* The same default-route trees in the packed layout (4 bytes per entry
+ * instead of 8, half the HBM writes, device-to-host copy and all-gather
+ * volume):
+ *   tree[i*V+v] = parent | port << 16   (parent, port as in sdnr_dfs_tables;
+ *                                         port 0xFFFF for the root),
+ *   tree[i*V+v] = 0xFFFFFFFF            v unreachable (SDNR_TREE_NONE).
+ * Needs V <= 65535 and every port in [0, 0xFFFE] -- OpenFlow 1.0 port
+ * numbers are 16-bit (ofp_phy_port.port_no) -- else SDNR_ERR_INVAL. */
+int sdnr_dfs_tables_packed(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc,
+                           uint32_t *tree, uint32_t flags);
 
 /* Shortest routes, find_route(src, dst, multiple=True) -> _find_routes_bfs
  * (topology_db.py:86-122, called from :168-180), as per-destination tables:

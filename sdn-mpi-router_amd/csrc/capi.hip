@@ -156,6 +156,7 @@ int sdnr_destroy(sdnr_ctx *ctx)
     (void)hipStreamSynchronize(ctx->stream);
     free_graph(ctx);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
+    if (ctx->scratch2) (void)hipFree(ctx->scratch2);
     if (ctx->stage) (void)hipFree(ctx->stage);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
@@ -191,11 +192,13 @@ int sdnr_graph_upload(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_pt
         return sdnr_fail(SDNR_ERR_INVAL, "graph_upload: row_ptr[0]=%d row_ptr[V]=%d, E=%d",
                          row_ptr[0], row_ptr[V], E);
     int32_t maxdeg = 0;
+    bool port16 = true;
     for (int32_t u = 0; u < V; ++u) {
         const int32_t a = row_ptr[u], b = row_ptr[u + 1];
         if (b < a) return sdnr_fail(SDNR_ERR_INVAL, "graph_upload: row_ptr decreases at %d", u);
         if (b - a > maxdeg) maxdeg = b - a;
         for (int32_t e = a; e < b; ++e) {
+            if (port[e] < 0 || port[e] >= 0xFFFF) port16 = false;
             if (col[e] < 0 || col[e] >= V)
                 return sdnr_fail(SDNR_ERR_INVAL, "graph_upload: col[%d]=%d out of range", e,
                                  col[e]);
@@ -295,6 +298,7 @@ int sdnr_graph_upload(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_pt
     ctx->E = E;
     ctx->W = W;
     ctx->max_deg = maxdeg;
+    ctx->port16 = port16;
     return SDNR_OK;
 }
 
@@ -346,7 +350,7 @@ int sdnr_dfs_tables(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc, int32_t *pa
     if (rc) return rc;
     if (nsrc > 0 && (!parent || !port))
         return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_tables: null table");
-    if (flags & SDNR_DEVICE_PTRS) return sdnr_launch_dfs(ctx, src, nsrc, parent, port, hops);
+    if (flags & SDNR_DEVICE_PTRS) return sdnr_launch_dfs(ctx, src, nsrc, parent, port, hops, nullptr);
     const size_t V = (size_t)ctx->V, rows = (size_t)nsrc * V;
     const size_t need = 4 * (size_t)nsrc + 256 + (rows * 4 + 256) * (hops ? 3 : 2);
     if ((rc = sdnr_reserve(&ctx->stage, &ctx->stage_bytes, need))) return rc;
@@ -356,10 +360,34 @@ int sdnr_dfs_tables(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc, int32_t *pa
     int32_t *d_prt = static_cast<int32_t *>(st.take(rows * 4));
     int32_t *d_hop = hops ? static_cast<int32_t *>(st.take(rows * 4)) : nullptr;
     SDNR_HIP(hipMemcpyAsync(d_src, src, 4 * (size_t)nsrc, hipMemcpyHostToDevice, ctx->stream));
-    if ((rc = sdnr_launch_dfs(ctx, d_src, nsrc, d_par, d_prt, d_hop))) return rc;
+    if ((rc = sdnr_launch_dfs(ctx, d_src, nsrc, d_par, d_prt, d_hop, nullptr))) return rc;
     SDNR_HIP(hipMemcpyAsync(parent, d_par, rows * 4, hipMemcpyDeviceToHost, ctx->stream));
     SDNR_HIP(hipMemcpyAsync(port, d_prt, rows * 4, hipMemcpyDeviceToHost, ctx->stream));
     if (hops) SDNR_HIP(hipMemcpyAsync(hops, d_hop, rows * 4, hipMemcpyDeviceToHost, ctx->stream));
+    SDNR_HIP(hipStreamSynchronize(ctx->stream));
+    return sdnr_check_watchdog(ctx);
+}
+
+int sdnr_dfs_tables_packed(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc, uint32_t *tree,
+                           uint32_t flags)
+{
+    int rc = begin_call(ctx, nsrc, src, flags, "sdnr_dfs_tables_packed");
+    if (rc) return rc;
+    if (nsrc > 0 && !tree) return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_tables_packed: null table");
+    if (ctx->V > 0xFFFF || !ctx->port16)
+        return sdnr_fail(SDNR_ERR_INVAL,
+                         "sdnr_dfs_tables_packed: needs V <= 65535 and ports < 0xFFFF (V=%d)",
+                         ctx->V);
+    if (flags & SDNR_DEVICE_PTRS) return sdnr_launch_dfs(ctx, src, nsrc, nullptr, nullptr, nullptr, tree);
+    const size_t V = (size_t)ctx->V, rows = (size_t)nsrc * V;
+    if ((rc = sdnr_reserve(&ctx->stage, &ctx->stage_bytes, 4 * (size_t)nsrc + 256 + rows * 4)))
+        return rc;
+    Stage st{static_cast<char *>(ctx->stage)};
+    int32_t *d_src = static_cast<int32_t *>(st.take(4 * (size_t)nsrc));
+    uint32_t *d_tree = static_cast<uint32_t *>(st.take(rows * 4));
+    SDNR_HIP(hipMemcpyAsync(d_src, src, 4 * (size_t)nsrc, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = sdnr_launch_dfs(ctx, d_src, nsrc, nullptr, nullptr, nullptr, d_tree))) return rc;
+    SDNR_HIP(hipMemcpyAsync(tree, d_tree, rows * 4, hipMemcpyDeviceToHost, ctx->stream));
     SDNR_HIP(hipStreamSynchronize(ctx->stream));
     return sdnr_check_watchdog(ctx);
 }

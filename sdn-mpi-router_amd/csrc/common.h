@@ -62,6 +62,9 @@ struct sdnr_ctx {
     size_t scratch_bytes = 0;
     void *stage = nullptr;
     size_t stage_bytes = 0;
+    void *scratch2 = nullptr;           // int32 tables behind a packed-table call
+    size_t scratch2_bytes = 0;
+    bool port16 = false;                // every port fits the packed layout (< 0xFFFF)
 
     // timing of the main kernel(s) of the last SDNR_TIMING call
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -94,7 +97,8 @@ int sdnr_check_watchdog(sdnr_ctx *ctx);   // after a stream sync
 // kernel launchers (dfs.hip, shortest.hip, apsp.hip); device pointers,
 // asynchronous on ctx->stream
 int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
-                    int32_t *d_parent, int32_t *d_port, int32_t *d_hops);
+                    int32_t *d_parent, int32_t *d_port, int32_t *d_hops,
+                    uint32_t *d_tree);        // d_tree: packed layout instead of the three
 int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
                          uint16_t *d_dist, int32_t *d_nh, int32_t *d_nh_port);
 int sdnr_launch_apsp(sdnr_ctx *ctx, uint16_t *d_dist);

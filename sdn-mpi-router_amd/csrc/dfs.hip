@@ -1052,7 +1052,7 @@ __global__ __launch_bounds__(64) void dfs_global_packed_kernel(
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int swz(int x) { return lds_swz(x); }   // common.h
 
-template <int NW, bool HOPS>
+template <int NW, bool HOPS, bool PACKED>
 __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
     int V, const uint16_t *__restrict__ adj, const uint16_t *__restrict__ radj,
     const uint32_t *__restrict__ deg, const int32_t *__restrict__ row_ptr,
@@ -1089,12 +1089,12 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
     for (int si = blockIdx.x; si < nsrc; si += gridDim.x) {
         const int s = uniform(src[si]);
         int32_t *prow = out_parent + (size_t)si * V;
-        int32_t *trow = out_port + (size_t)si * V;
+        int32_t *trow = PACKED ? nullptr : out_port + (size_t)si * V;
         int32_t *hrow = HOPS ? out_hops + (size_t)si * V : nullptr;
         if (s < 0 || s >= V) {
             for (int v = threadIdx.x; v < V; v += blockDim.x) {
-                prow[v] = -1;
-                trow[v] = -1;
+                prow[v] = -1;                    // packed: 0xFFFFFFFF
+                if (!PACKED) trow[v] = -1;
                 if (HOPS) hrow[v] = -1;
             }
             continue;
@@ -1312,8 +1312,13 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             for (int k = 0; k < U; ++k) {
                 const int v = v0 + k * (int)blockDim.x;
                 if (v < V) {
-                    prow[v] = p[k];
-                    trow[v] = pt[k];
+                    if (PACKED) {                // parent | port << 16, -1 -> 0xFFFF
+                        prow[v] = (int32_t)(((uint32_t)p[k] & 0xFFFFu) |
+                                            ((uint32_t)pt[k] << 16));
+                    } else {
+                        prow[v] = p[k];
+                        trow[v] = pt[k];
+                    }
                     if (HOPS) hrow[v] = p[k] < 0 ? -1 : (v == s ? 0 : (int)dep[v]);
                 }
             }
@@ -1336,6 +1341,16 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
         atomicMax(&g_stamp[12], ~kstart);
     }
 #endif
+}
+
+// packed tables from int32 ones (strategies without a packed epilogue)
+__global__ __launch_bounds__(256) void dfs_pack_kernel(size_t n, const int32_t *__restrict__ parent,
+                                                       const int32_t *__restrict__ port,
+                                                       uint32_t *__restrict__ tree)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        tree[i] = ((uint32_t)parent[i] & 0xFFFFu) | ((uint32_t)port[i] << 16);
 }
 
 template <typename Kern>
@@ -1523,10 +1538,11 @@ static int dfs_batch_depth(const sdnr_ctx *ctx)
 }
 
 int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
-                    int32_t *d_parent, int32_t *d_port, int32_t *d_hops)
+                    int32_t *d_parent, int32_t *d_port, int32_t *d_hops, uint32_t *d_tree)
 {
     const int V = ctx->V;
     if (nsrc == 0 || V == 0) return SDNR_OK;
+    const bool packed = d_tree != nullptr;
     const bool ell = ctx->W > 0;
     const bool hops = d_hops != nullptr;
     const bool narrow = ctx->max_deg <= SDNR_WAVE;     // one row = one wavefront
@@ -1567,6 +1583,19 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
                           dfs_lds_bytes_count(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;
     const bool async_ok = count_ok && dfs_lds_bytes_async(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;
     const bool async = async_ok && (force ? !strcmp(force, "async") : small);
+    if (packed && !async) {
+        // no packed epilogue in this strategy: int32 tables into scratch, then pack
+        const size_t n = (size_t)nsrc * (size_t)V;
+        int rc = sdnr_reserve(&ctx->scratch2, &ctx->scratch2_bytes, 2 * n * sizeof(int32_t));
+        if (rc) return rc;
+        int32_t *tp = static_cast<int32_t *>(ctx->scratch2);
+        if ((rc = sdnr_launch_dfs(ctx, d_src, nsrc, tp, tp + n, nullptr, nullptr))) return rc;
+        hipLaunchKernelGGL(dfs_pack_kernel, dim3(ctx->num_cus * 8), dim3(256), 0, ctx->stream, n,
+                           tp, tp + n, d_tree);
+        SDNR_HIP(hipGetLastError());
+        if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+        return SDNR_OK;
+    }
     const bool count = !async && count_ok && (force ? !strcmp(force, "count") : small);
     const bool coop_ok = ctx->adj16 != nullptr && V < 65535 &&
                          dfs_lds_bytes_coop(V) <= SDNR_MAX_LDS_PER_BLOCK;
@@ -1584,15 +1613,21 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
                                       "dfs_async_kernel<4>", "dfs_async_kernel<5>",
                                       "dfs_async_kernel<6>"};
         ctx->last_kernel = names[nw];
-#define SDNR_ASYNC(N_, H_)                                                                   \
+#define SDNR_ASYNC_P(N_, H_, P_)                                                             \
     do {                                                                                     \
-        auto k = dfs_async_kernel<N_, H_>;                                                   \
+        auto k = dfs_async_kernel<N_, H_, P_>;                                               \
         allow_full_lds(k);                                                                   \
         hipLaunchKernelGGL(k, dim3(cgrid), dim3(N_ * 64), cl, ctx->stream, V, ctx->adj16,    \
                            ctx->radj16, ctx->deg32, ctx->row_ptr, ctx->port, ctx->W,         \
-                           ctx->ell_port, d_src, nsrc, d_parent, d_port, d_hops, err);       \
+                           ctx->ell_port, d_src, nsrc,                                       \
+                           P_ ? reinterpret_cast<int32_t *>(d_tree) : d_parent, d_port,      \
+                           d_hops, err);                                                     \
     } while (0)
-        if (nw == 2) {
+#define SDNR_ASYNC(N_, H_) SDNR_ASYNC_P(N_, H_, false)
+        if (packed) {
+            ctx->last_kernel = "dfs_async_kernel<4,packed>";
+            SDNR_ASYNC_P(4, false, true);
+        } else if (nw == 2) {
             if (hops) SDNR_ASYNC(2, true); else SDNR_ASYNC(2, false);
         } else if (nw == 3) {
             if (hops) SDNR_ASYNC(3, true); else SDNR_ASYNC(3, false);
@@ -1604,6 +1639,7 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
             if (hops) SDNR_ASYNC(4, true); else SDNR_ASYNC(4, false);
         }
 #undef SDNR_ASYNC
+#undef SDNR_ASYNC_P
     } else if (count) {
         const size_t cl = dfs_lds_bytes_count(V, hops);
         size_t cpc = SDNR_LDS_PER_CU / cl;

@@ -16,8 +16,8 @@ import threading
 import numpy as np
 
 __all__ = ["NativeUnavailable", "SdnrError", "library", "library_path",
-           "Context", "DEVICE_PTRS", "TIMING", "UNREACHED", "DIST_INF",
-           "EXPORTED_SYMBOLS"]
+           "Context", "DEVICE_PTRS", "TIMING", "UNREACHED", "DIST_INF", "TREE_NONE",
+           "EXPORTED_SYMBOLS", "unpack_tree"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_NAME = "libsdnroute.so"
@@ -26,13 +26,15 @@ DEVICE_PTRS = 0x1
 TIMING = 0x2
 UNREACHED = -1
 DIST_INF = 0xFFFF
+TREE_NONE = 0xFFFFFFFF
 ABI_VERSION = 1
 
 # every entry point declared in include/sdnroute.h
 EXPORTED_SYMBOLS = (
     "sdnr_abi_version", "sdnr_last_error", "sdnr_device_count", "sdnr_create",
     "sdnr_destroy", "sdnr_set_stream", "sdnr_synchronize", "sdnr_graph_upload",
-    "sdnr_graph_info", "sdnr_dfs_tables", "sdnr_shortest_tables", "sdnr_apsp",
+    "sdnr_graph_info", "sdnr_dfs_tables", "sdnr_dfs_tables_packed", "sdnr_shortest_tables",
+    "sdnr_apsp",
     "sdnr_last_kernel_ms", "sdnr_last_kernel",
 )
 
@@ -69,6 +71,7 @@ def _bind(L):
         "sdnr_graph_info": ([vp, ctypes.POINTER(i32), ctypes.POINTER(i32),
                              ctypes.POINTER(i32)], c_int),
         "sdnr_dfs_tables": ([vp, vp, i32, vp, vp, vp, u32], c_int),
+        "sdnr_dfs_tables_packed": ([vp, vp, i32, vp, u32], c_int),
         "sdnr_shortest_tables": ([vp, vp, i32, vp, vp, vp, u32], c_int),
         "sdnr_apsp": ([vp, vp, u32], c_int),
         "sdnr_last_kernel_ms": ([vp, ctypes.POINTER(ctypes.c_float)], c_int),
@@ -118,6 +121,17 @@ def device_count():
     n = ctypes.c_int(0)
     _check(library().sdnr_device_count(ctypes.byref(n)))
     return n.value
+
+
+def unpack_tree(tree):
+    """Packed tree rows -> (parent, port) int32, -1 where the packed half is
+    0xFFFF (unreached vertex / the root's port)."""
+    t = np.asarray(tree, np.uint32)
+    parent = (t & 0xFFFF).astype(np.int32)
+    port = (t >> 16).astype(np.int32)
+    parent[parent == 0xFFFF] = -1
+    port[port == 0xFFFF] = -1
+    return parent, port
 
 
 def _ptr(a):
@@ -188,6 +202,14 @@ class Context(object):
                                          _ptr(port), _ptr(hops), 0))
         return parent, port, hops
 
+    def dfs_tables_packed(self, srcs):
+        """Packed trees: uint32 [S, V], parent | port << 16 (see unpack_tree)."""
+        srcs = np.ascontiguousarray(srcs, np.int32)
+        S, V = int(srcs.shape[0]), self.V
+        tree = np.empty((S, V), np.uint32)
+        _check(self._lib.sdnr_dfs_tables_packed(self._h, _ptr(srcs), S, _ptr(tree), 0))
+        return tree
+
     def shortest_tables(self, dsts, with_nexthop=True):
         dsts = np.ascontiguousarray(dsts, np.int32)
         D, V = int(dsts.shape[0]), self.V
@@ -211,6 +233,11 @@ class Context(object):
             self._h, ctypes.c_void_p(src_ptr), int(nsrc), ctypes.c_void_p(parent_ptr),
             ctypes.c_void_p(port_ptr), ctypes.c_void_p(hops_ptr) if hops_ptr else None,
             flags))
+
+    def dfs_tables_packed_device(self, src_ptr, nsrc, tree_ptr, timing=False):
+        flags = DEVICE_PTRS | (TIMING if timing else 0)
+        _check(self._lib.sdnr_dfs_tables_packed(self._h, ctypes.c_void_p(src_ptr), int(nsrc),
+                                                ctypes.c_void_p(tree_ptr), flags))
 
     def shortest_tables_device(self, dst_ptr, ndst, dist_ptr, nh_ptr=0, nh_port_ptr=0,
                                timing=False):

@@ -73,6 +73,48 @@ def test_dfs_small_all_sources(ctx, monkeypatch, name, strategy, ell):
     _check_pairs(g, fabric, p, t, srcs)
 
 
+def _pack(p, t):
+    return ((p.astype(np.int64) & 0xFFFF) | ((t.astype(np.int64) & 0xFFFF) << 16)).astype(np.uint32)
+
+
+@pytest.mark.parametrize("strategy", ["auto", "lds", "global"])
+@pytest.mark.parametrize("name", ["mock", "fat_tree_k8", "dragonfly_a4_h2_p2", "random_V40",
+                                  "jellyfish_n60_r5", "torus_5x3x2"])
+def test_dfs_packed_small(ctx, monkeypatch, name, strategy):
+    _strategy(monkeypatch, None if strategy == "auto" else strategy)
+    csr = G.Golden(name).fabric().csr()
+    srcs = np.arange(csr.V, dtype=np.int32)
+    ctx.upload(csr)
+    tree = ctx.dfs_tables_packed(srcs)
+    po, to, _ = O.dfs_tables(csr, srcs, with_hops=False, nthreads=NTHREADS)
+    np.testing.assert_array_equal(tree, _pack(po, to))
+    p, t = _native.unpack_tree(tree)
+    np.testing.assert_array_equal(p, po)
+    np.testing.assert_array_equal(t, to)
+
+
+def test_dfs_packed_fullsize_k48(ctx):
+    fabric = T.fat_tree(48)
+    csr = fabric.csr()
+    srcs = np.unique(fabric.host_table()[0]).astype(np.int32)
+    ctx.upload(csr)
+    tree = ctx.dfs_tables_packed(srcs)
+    assert ctx.last_kernel() == "dfs_async_kernel<4,packed>"
+    po, to, _ = O.dfs_tables(csr, srcs, with_hops=False, nthreads=NTHREADS)
+    np.testing.assert_array_equal(tree, _pack(po, to))
+
+
+def test_dfs_packed_rejects_wide_ports(ctx):
+    from sdnmpi_amd.topologies import CSR
+    c = CSR(np.array([1, 2]), np.array([0, 1, 2]), np.array([1, 0]), np.array([0xFFFF, 3]))
+    ctx.upload(c)
+    with pytest.raises(_native.SdnrError) as ei:
+        ctx.dfs_tables_packed(np.array([0], np.int32))
+    assert ei.value.code == -22
+    p, t, _ = ctx.dfs_tables(np.array([0], np.int32))      # int32 layout still works
+    assert t[0, 1] == 0xFFFF
+
+
 def test_dfs_without_hops_and_repeated_sources(ctx):
     csr = T.fat_tree(8).csr()
     srcs = np.array([5, 5, 0, csr.V - 1, 17, 5], np.int32)

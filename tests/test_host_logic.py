@@ -119,3 +119,11 @@ def test_shortest_paths_lex_matches_reference_order():
             assert seqs == sorted(seqs)
             for q in seqs:
                 assert len(q) - 1 == dist[d, s] and len(set(q)) == len(q)
+
+
+def test_unpack_tree_layout():
+    from sdnmpi_amd._native import unpack_tree
+    t = np.array([[0x00030002, 0xFFFF0005, 0xFFFFFFFF, 0xFFFE0000]], np.uint32)
+    p, q = unpack_tree(t)
+    assert p.tolist() == [[2, 5, -1, 0]]
+    assert q.tolist() == [[3, -1, -1, 0xFFFE]]
