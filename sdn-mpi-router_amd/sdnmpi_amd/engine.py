@@ -52,6 +52,32 @@ class TableCache(object):
         self.dfs = None            # (parent, port, hops)
         self.sp_row = {}           # destination vertex -> row
         self.sp = None             # (dist, nh, nh_port)
+        self.rows_computed = 0     # rows sent to the GPU (both modes)
+        self.rows_inherited = 0    # rows kept across a graph change
+
+    def inherit(self, old, diff):
+        """Keep the rows of ``old`` (a cache of the previous graph over the
+        same vertex set) that the link changes in ``diff`` cannot alter
+        (:mod:`sdnmpi_amd.incremental`); the rest are recomputed on demand."""
+        from .incremental import dfs_rows_affected, sp_rows_affected
+        if old.dfs is not None and old.dfs[2] is not None:
+            srcs = np.empty(len(old.dfs_row), np.int64)
+            for v, r in old.dfs_row.items():
+                srcs[r] = v
+            keep = ~dfs_rows_affected(old.dfs[0], old.dfs[2], srcs, diff)
+            if keep.any():
+                self.dfs = tuple(a[keep] for a in old.dfs)
+                self.dfs_row = {int(v): i for i, v in enumerate(srcs[keep].tolist())}
+                self.rows_inherited += int(keep.sum())
+        if old.sp is not None and old.sp[1] is not None:
+            dsts = np.empty(len(old.sp_row), np.int64)
+            for v, r in old.sp_row.items():
+                dsts[r] = v
+            keep = ~sp_rows_affected(old.sp[0], old.sp[1], diff)
+            if keep.any():
+                self.sp = tuple(a[keep] for a in old.sp)
+                self.sp_row = {int(v): i for i, v in enumerate(dsts[keep].tolist())}
+                self.rows_inherited += int(keep.sum())
 
     @staticmethod
     def _append(old, new):
@@ -65,6 +91,7 @@ class TableCache(object):
                    if v not in self.dfs_row]
         if missing:
             tabs = engine.dfs_tables(self.export, np.asarray(missing, np.int32))
+            self.rows_computed += len(missing)
             base = 0 if self.dfs is None else self.dfs[0].shape[0]
             self.dfs = self._append(self.dfs, tabs)
             for i, v in enumerate(missing):
@@ -76,6 +103,7 @@ class TableCache(object):
                    if v not in self.sp_row]
         if missing:
             tabs = engine.shortest_tables(self.export, np.asarray(missing, np.int32))
+            self.rows_computed += len(missing)
             base = 0 if self.sp is None else self.sp[0].shape[0]
             self.sp = self._append(self.sp, tabs)
             for i, v in enumerate(missing):

@@ -25,6 +25,7 @@ import numpy as np
 
 from ..engine import RouteEngine, TableCache, shortest_paths_lex, tree_path
 from ..graph import TrackedDict, Versions, export_graph
+from ..incremental import edge_diff
 
 try:   # the reference takes OFPP_LOCAL from Ryu's OpenFlow 1.0 module (:5)
     from ryu.ofproto.ofproto_v1_0 import OFPP_LOCAL
@@ -44,16 +45,21 @@ class TopologyDB(object):
     ``batch_sources``: when a table must be computed, compute it for every
     host-bearing switch at once (the all-pairs batch) instead of only the
     switch asked about.
+    ``incremental``: after a link change over the same switch set, keep the
+    cached rows the change cannot alter (:mod:`sdnmpi_amd.incremental`) and
+    recompute only the others.
     """
 
-    def __init__(self, engine=None, device=0, batch_sources=True):
+    def __init__(self, engine=None, device=0, batch_sources=True, incremental=True):
         super(TopologyDB, self).__init__()
         self._versions = Versions()
         self._engine = engine
         self._device = device
         self._batch = batch_sources
+        self._incremental = incremental
         self._export = None
         self._cache = None
+        self._hv = (None, None)          # (version key, host vertices)
         # Switch DPID -> Switch; src DPID -> dst DPID -> Link; MAC -> Host
         self.switches = {}
         self.links = {}
@@ -132,22 +138,31 @@ class TopologyDB(object):
             if ex is not None and _same_graph(ex.csr, new.csr):
                 ex.key = key             # only host ports / MACs changed
             else:
+                old = self._cache
                 self._export = ex = new
                 self._cache = TableCache(new)
+                if self._incremental and old is not None:
+                    diff = edge_diff(old.export.csr, new.csr)
+                    if diff is not None:
+                        self._cache.inherit(old, diff)
         return ex
 
     def _host_vertices(self, ex):
-        idx = ex.index
-        return sorted({idx[h.port.dpid] for h in self.hosts.values()})
+        key = self._versions.key()
+        if self._hv[0] != key:
+            idx = ex.index
+            self._hv = (key, sorted({idx[h.port.dpid] for h in self.hosts.values()}))
+        return self._hv[1]
 
     def _dfs(self, ex, s):
-        batch = self._host_vertices(ex) if self._batch and self._cache.dfs is None else ()
-        tabs = self._cache.dfs_rows(self.engine, [s], batch)
-        r = self._cache.dfs_row[s]
+        c = self._cache
+        batch = self._host_vertices(ex) if self._batch and s not in c.dfs_row else ()
+        tabs = c.dfs_rows(self.engine, [s], batch)
+        r = c.dfs_row[s]
         return tabs[0][r], tabs[1][r]
 
     def _dist(self, ex, d):
-        batch = self._host_vertices(ex) if self._batch and self._cache.sp is None else ()
+        batch = self._host_vertices(ex) if self._batch and d not in self._cache.sp_row else ()
         tabs = self._cache.sp_rows(self.engine, [d], batch)
         return tabs[0][self._cache.sp_row[d]]
 

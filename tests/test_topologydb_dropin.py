@@ -210,3 +210,50 @@ def test_tracked_dicts_are_dicts():
     v = db._versions.key()
     db.links[9].pop(1)
     assert db._versions.key() != v
+
+
+def _link_failure_replay(db, fabric):
+    """Routes for every host pair, then a failed agg-core link (Ryu reports
+    both directions) and a re-added one; every route must equal the
+    reference semantics on the mutated dicts, and only the affected
+    sources may be recomputed."""
+    from oracle import oracle as O
+    macs = fabric.host_macs()
+    pairs = [(a, b) for a in macs[::5] for b in macs[::3]]
+    assert db.find_routes(pairs) == [O.find_route_pair(db, a, b) for a, b in pairs]
+    hosts = len(set(h.port.dpid for h in db.hosts.values()))
+    # a tree link of the first source's table: agg -> core 0 where core 0
+    # (dpid 1) was first pushed
+    t = db.route_tables("dfs")
+    dp = t["dpids"]
+    a = int(dp[t["parent"][0][0]])     # vertex 0 = core 0
+    ab = db.links[a][1]
+    ba = db.links[1][a]
+    db.delete_link(ab)
+    db.delete_link(ba)
+    got = db.find_routes(pairs)
+    assert got == [O.find_route_pair(db, a, b) for a, b in pairs]
+    c = db._cache
+    assert 0 < c.rows_computed < hosts and c.rows_inherited > 0
+    db.add_link(ab)
+    db.add_link(ba)
+    assert db.find_routes(pairs) == [O.find_route_pair(db, a, b) for a, b in pairs]
+    assert db._cache.rows_computed < hosts
+    # shortest mode keeps its rows across the change too
+    sp = [db.find_route(a, b, True) for a, b in pairs[:40]]
+    assert sp == [O.find_routes_all_shortest(db, a, b) for a, b in pairs[:40]]
+
+
+def test_link_failure_incremental_fake_engine():
+    from sdnmpi_amd import topologies as T
+    fabric = T.fat_tree(8)
+    db = fabric.populate(TopologyDB())
+    db._engine = _FakeEngine()
+    _link_failure_replay(db, fabric)
+
+
+@pytest.mark.gpu
+def test_link_failure_incremental_gpu():
+    from sdnmpi_amd import topologies as T
+    fabric = T.fat_tree(8)
+    _link_failure_replay(fabric.populate(TopologyDB()), fabric)
