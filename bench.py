@@ -53,7 +53,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--fabric", default="fat_tree:48")
-    ap.add_argument("--mode", choices=["dfs", "shortest"], default="dfs")
+    ap.add_argument("--mode", choices=["dfs", "shortest", "flows"], default="dfs")
+    ap.add_argument("--ranks", type=int, default=1024,
+                    help="flows mode: MPI ranks placed on random hosts; every ordered "
+                         "rank pair's flow entries are emitted per step")
     ap.add_argument("--layout", choices=["auto", "packed", "int32"], default="auto",
                     help="dfs tables: packed u32 (parent | port << 16) when the fabric "
                          "allows it (V <= 65535, 16-bit ports), else int32 parent + port")
@@ -127,6 +130,112 @@ class _DictDB(object):
         self.hosts[h.mac] = h
 
 
+def main_flows(args, world, rank, local, dev):
+    """Flow-entry emission: for R ranks on seeded random
+    hosts, every ordered rank pair's fdb (Router._add_flows_for_path,
+    reference sdnmpi/router.py:83-104) from default-route tables already
+    resident in HBM.  One step = offsets (lengths + scan) + the tree walks
+    for this rank's share of the pairs; value = pairs per second."""
+    fabric = T.by_name(args.fabric)
+    csr = fabric.csr()
+    V = csr.V
+    hv, hp = fabric.host_table()
+    rng = np.random.default_rng(7)
+    R = min(args.ranks, fabric.n_hosts)
+    host = rng.choice(fabric.n_hosts, R, replace=False)
+    srcs = np.unique(hv[host]).astype(np.int32)
+    row_of = {int(v): i for i, v in enumerate(srcs.tolist())}
+    a_idx = np.repeat(np.arange(R), R)
+    b_idx = np.tile(np.arange(R), R)
+    npairs_all = R * R
+    lo, hi, _ = D.shard_bounds(npairs_all, world, rank)
+    rows = np.asarray([row_of[int(v)] for v in hv[host[a_idx[lo:hi]]]], np.int32)
+    dsts = hv[host[b_idx[lo:hi]]].astype(np.int32)
+    last = hp[host[b_idx[lo:hi]]].astype(np.int32)
+    n = hi - lo
+
+    ctx = _native.Context(local)
+    ctx.upload(csr)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream.cuda_stream)
+    S = len(srcs)
+    t_src = torch.from_numpy(srcs).to(dev)
+    par = torch.empty((S, V), dtype=torch.int32, device=dev)
+    prt = torch.empty_like(par)
+    hop = torch.empty_like(par)
+    ctx.dfs_tables_device(t_src.data_ptr(), S, par.data_ptr(), prt.data_ptr(), hop.data_ptr())
+    t_rows = torch.from_numpy(rows).to(dev)
+    t_dsts = torch.from_numpy(dsts).to(dev)
+    t_last = torch.from_numpy(last).to(dev)
+    off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    ctx.route_offsets_device(hop.data_ptr(), t_rows.data_ptr(), t_dsts.data_ptr(), n, off.data_ptr())
+    torch.cuda.synchronize(dev)
+    total = int(off[-1].item())
+    sw = torch.empty(total, dtype=torch.int32, device=dev)
+    hpo = torch.empty(total, dtype=torch.int32, device=dev)
+
+    def step(timing=False):
+        ctx.route_offsets_device(hop.data_ptr(), t_rows.data_ptr(), t_dsts.data_ptr(), n,
+                                 off.data_ptr())
+        ctx.expand_routes_device(par.data_ptr(), prt.data_ptr(), t_rows.data_ptr(),
+                                 t_dsts.data_ptr(), t_last.data_ptr(), n, off.data_ptr(),
+                                 sw.data_ptr(), hpo.data_ptr(), timing=timing)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    kms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(timing=True)
+        kms.append(ctx.last_kernel_ms())        # waits for this step's walk kernel
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed / args.steps * 1e3
+    kern_ms = float(np.mean(kms))
+    # walk kernel: per entry parent + port read (8 B) and (switch, port)
+    # written (8 B); per pair row/dst/last_port (12 B) + offsets pair (16 B)
+    bytes_launch = 16 * total + 28 * n
+    achieved = bytes_launch / (kern_ms / 1e3) / 1e9
+    traffic = None
+    if os.path.exists(TRAFFIC_FILE):
+        try:
+            traffic = json.load(open(TRAFFIC_FILE)).get("%s/flows/N%d" % (args.fabric, world))
+        except Exception:   # noqa: BLE001
+            traffic = None
+    out = {
+        "metric": "flow entries for all MPI rank pairs (Router._add_flows_for_path), pairs/sec",
+        "value": float(npairs_all) / (ms / 1e3), "unit": "routes/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int32",
+        "data": "synthetic (canonical fabric, ranks on seeded random hosts)",
+        "config": {"workload": "%s flow entries of %d ranks (%d ordered pairs)" % (
+            args.fabric, R, npairs_all), "fabric": args.fabric, "ranks": R,
+            "pairs": npairs_all, "entries": total * world, "sources": S,
+            "parallelism": "pairs sharded over %d GPU(s)" % world},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "route_walk_kernel", "kernel_ms": kern_ms,
+                     "bytes_per_launch": bytes_launch},
+        "entries_per_s": float(total) * world / (ms / 1e3),
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -136,6 +245,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if args.mode == "flows":
+        return main_flows(args, world, rank, local, dev)
 
     fabric = T.by_name(args.fabric)
     csr = fabric.csr()

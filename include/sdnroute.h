@@ -130,6 +130,29 @@ int sdnr_shortest_tables(sdnr_ctx *ctx, const int32_t *dst, int32_t ndst,
  * V <= 16384. */
 int sdnr_apsp(sdnr_ctx *ctx, uint16_t *dist, uint32_t flags);
 
+/* Flow entries of many host pairs from default-route tables (the OFPFlowMods
+ * Router._add_flows_for_path installs, reference sdnmpi/router.py:83-104,
+ * for the fdb _route_to_fdb builds, sdnmpi/util/topology_db.py:127-138).
+ * Tables: row-major [nrows][V] as returned by sdnr_dfs_tables (hops needed
+ * for the sizes).  Pair i is (row rows[i] = its source's tree, destination
+ * switch dsts[i], last_port[i] = the destination host's port or OFPP_LOCAL).
+ *
+ * sdnr_route_offsets: offsets[0..npairs] (int64), offsets[i+1]-offsets[i] =
+ *   entries of pair i = hops + 1 (0 if unreachable); offsets[npairs] = total.
+ * sdnr_route_expand: for pair i, entries offsets[i]..offsets[i+1]-1 in path
+ *   order: hop_switch[j] = dense switch id, hop_port[j] = its out port; the
+ *   last entry is (dsts[i], last_port[i]).  Bit-identical to find_route's
+ *   fdb with switch ids mapped to dpids.
+ * Host buffers: the tables are staged per call (nrows * V entries each). */
+int sdnr_route_offsets(sdnr_ctx *ctx, const int32_t *hops, int32_t nrows,
+                       const int32_t *rows, const int32_t *dsts, int32_t npairs,
+                       int64_t *offsets, uint32_t flags);
+int sdnr_route_expand(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port,
+                      int32_t nrows, const int32_t *rows, const int32_t *dsts,
+                      const int32_t *last_port, int32_t npairs,
+                      const int64_t *offsets, int32_t *hop_switch,
+                      int32_t *hop_port, uint32_t flags);
+
 /* Device time in milliseconds of the main kernel(s) of the last table call
  * made with SDNR_TIMING (waits for that call to finish). */
 int sdnr_last_kernel_ms(sdnr_ctx *ctx, float *ms);

@@ -435,6 +435,98 @@ int sdnr_apsp(sdnr_ctx *ctx, uint16_t *dist, uint32_t flags)
     return SDNR_OK;
 }
 
+static int check_pairs(const sdnr_ctx *ctx, int32_t nrows, const int32_t *rows,
+                       const int32_t *dsts, int32_t npairs, const char *fn)
+{
+    for (int32_t i = 0; i < npairs; ++i) {
+        if (rows[i] < 0 || rows[i] >= nrows)
+            return sdnr_fail(SDNR_ERR_INVAL, "%s: row[%d]=%d outside [0,%d)", fn, i, rows[i], nrows);
+        if (dsts[i] < 0 || dsts[i] >= ctx->V)
+            return sdnr_fail(SDNR_ERR_INVAL, "%s: dst[%d]=%d outside [0,%d)", fn, i, dsts[i], ctx->V);
+    }
+    return SDNR_OK;
+}
+
+int sdnr_route_offsets(sdnr_ctx *ctx, const int32_t *hops, int32_t nrows, const int32_t *rows,
+                       const int32_t *dsts, int32_t npairs, int64_t *offsets, uint32_t flags)
+{
+    int rc = begin_call(ctx, 0, nullptr, flags, "sdnr_route_offsets");
+    if (rc) return rc;
+    if (npairs < 0 || nrows < 0 || !offsets || (npairs > 0 && (!hops || !rows || !dsts)))
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_route_offsets: bad arguments");
+    if (flags & SDNR_DEVICE_PTRS)
+        return sdnr_launch_route_offsets(ctx, hops, rows, dsts, npairs, offsets);
+    if ((rc = check_pairs(ctx, nrows, rows, dsts, npairs, "sdnr_route_offsets"))) return rc;
+    const size_t tab = (size_t)nrows * ctx->V * 4, pr = (size_t)npairs * 4;
+    if ((rc = sdnr_reserve(&ctx->stage, &ctx->stage_bytes,
+                           tab + 2 * pr + ((size_t)npairs + 1) * 8 + 1024)))
+        return rc;
+    Stage st{static_cast<char *>(ctx->stage)};
+    int32_t *d_h = static_cast<int32_t *>(st.take(tab));
+    int32_t *d_r = static_cast<int32_t *>(st.take(pr));
+    int32_t *d_d = static_cast<int32_t *>(st.take(pr));
+    int64_t *d_o = static_cast<int64_t *>(st.take(((size_t)npairs + 1) * 8));
+    SDNR_HIP(hipMemcpyAsync(d_h, hops, tab, hipMemcpyHostToDevice, ctx->stream));
+    SDNR_HIP(hipMemcpyAsync(d_r, rows, pr, hipMemcpyHostToDevice, ctx->stream));
+    SDNR_HIP(hipMemcpyAsync(d_d, dsts, pr, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = sdnr_launch_route_offsets(ctx, d_h, d_r, d_d, npairs, d_o))) return rc;
+    SDNR_HIP(hipMemcpyAsync(offsets, d_o, ((size_t)npairs + 1) * 8, hipMemcpyDeviceToHost,
+                            ctx->stream));
+    SDNR_HIP(hipStreamSynchronize(ctx->stream));
+    return SDNR_OK;
+}
+
+int sdnr_route_expand(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port, int32_t nrows,
+                      const int32_t *rows, const int32_t *dsts, const int32_t *last_port,
+                      int32_t npairs, const int64_t *offsets, int32_t *hop_switch,
+                      int32_t *hop_port, uint32_t flags)
+{
+    int rc = begin_call(ctx, 0, nullptr, flags, "sdnr_route_expand");
+    if (rc) return rc;
+    if (npairs < 0 || nrows < 0 || !offsets ||
+        (npairs > 0 && (!parent || !port || !rows || !dsts || !last_port)))
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_route_expand: bad arguments");
+    if (flags & SDNR_DEVICE_PTRS)
+        return sdnr_launch_route_expand(ctx, parent, port, rows, dsts, last_port, npairs, offsets,
+                                        hop_switch, hop_port);
+    if ((rc = check_pairs(ctx, nrows, rows, dsts, npairs, "sdnr_route_expand"))) return rc;
+    const int64_t total = offsets[npairs];
+    if (total > 0 && (!hop_switch || !hop_port))
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_route_expand: null output");
+    for (int32_t i = 0; i < npairs; ++i)
+        if (offsets[i + 1] < offsets[i] || offsets[i] < 0)
+            return sdnr_fail(SDNR_ERR_INVAL, "sdnr_route_expand: offsets not ascending at %d", i);
+    const size_t tab = (size_t)nrows * ctx->V * 4, pr = (size_t)npairs * 4;
+    const size_t ent = (size_t)total * 4;
+    if ((rc = sdnr_reserve(&ctx->stage, &ctx->stage_bytes,
+                           2 * tab + 3 * pr + ((size_t)npairs + 1) * 8 + 2 * ent + 2048)))
+        return rc;
+    Stage st{static_cast<char *>(ctx->stage)};
+    int32_t *d_p = static_cast<int32_t *>(st.take(tab));
+    int32_t *d_t = static_cast<int32_t *>(st.take(tab));
+    int32_t *d_r = static_cast<int32_t *>(st.take(pr));
+    int32_t *d_d = static_cast<int32_t *>(st.take(pr));
+    int32_t *d_l = static_cast<int32_t *>(st.take(pr));
+    int64_t *d_o = static_cast<int64_t *>(st.take(((size_t)npairs + 1) * 8));
+    int32_t *d_s = static_cast<int32_t *>(st.take(ent));
+    int32_t *d_q = static_cast<int32_t *>(st.take(ent));
+    SDNR_HIP(hipMemcpyAsync(d_p, parent, tab, hipMemcpyHostToDevice, ctx->stream));
+    SDNR_HIP(hipMemcpyAsync(d_t, port, tab, hipMemcpyHostToDevice, ctx->stream));
+    SDNR_HIP(hipMemcpyAsync(d_r, rows, pr, hipMemcpyHostToDevice, ctx->stream));
+    SDNR_HIP(hipMemcpyAsync(d_d, dsts, pr, hipMemcpyHostToDevice, ctx->stream));
+    SDNR_HIP(hipMemcpyAsync(d_l, last_port, pr, hipMemcpyHostToDevice, ctx->stream));
+    SDNR_HIP(hipMemcpyAsync(d_o, offsets, ((size_t)npairs + 1) * 8, hipMemcpyHostToDevice,
+                            ctx->stream));
+    if ((rc = sdnr_launch_route_expand(ctx, d_p, d_t, d_r, d_d, d_l, npairs, d_o, d_s, d_q)))
+        return rc;
+    if (ent) {
+        SDNR_HIP(hipMemcpyAsync(hop_switch, d_s, ent, hipMemcpyDeviceToHost, ctx->stream));
+        SDNR_HIP(hipMemcpyAsync(hop_port, d_q, ent, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    SDNR_HIP(hipStreamSynchronize(ctx->stream));
+    return SDNR_OK;
+}
+
 const char *sdnr_last_kernel(const sdnr_ctx *ctx) { return ctx ? ctx->last_kernel : ""; }
 
 int sdnr_last_kernel_ms(sdnr_ctx *ctx, float *ms)

@@ -1,0 +1,179 @@
+// routes.hip -- flow-entry emission from the default-route tables.
+//
+// SURVEY.md 8(f) 1.  The router installs, for a (src, dst) host pair, one
+// OFPFlowMod per switch of find_route(src, dst) (reference
+// sdnmpi/router.py:83-104, _add_flows_for_path), and find_route's fdb is the
+// tree path of the source's table turned into (switch, out port) pairs by
+// _route_to_fdb (sdnmpi/util/topology_db.py:127-138): one entry per hop with
+// the port toward the next switch, then the destination switch with the
+// host's port (or OFPP_LOCAL).  Batched over many pairs -- every MPI rank
+// pair of a job -- that is a ragged array:
+//   offsets[i] .. offsets[i+1]   entries of pair i (0 if unreachable),
+//   hop_switch[j], hop_port[j]   dense switch id and out port of entry j.
+// Pass 1 (route_len_kernel + a three-phase scan) sizes every pair from the
+// hop table; pass 2 (route_walk_kernel) walks each pair's tree path from the
+// destination up, writing entries back to front.  The tree rows stay L2 /
+// Infinity-Cache resident; the output is written once, in order.
+#include "common.h"
+
+namespace {
+
+constexpr int kScanThreads = 1024;
+constexpr int kScanItems = 8;
+constexpr int kScanTile = kScanThreads * kScanItems;
+
+__global__ __launch_bounds__(256) void route_len_kernel(
+    int V, const int32_t *__restrict__ hops, const int32_t *__restrict__ rows,
+    const int32_t *__restrict__ dsts, int npairs, int64_t *__restrict__ len)
+{
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += gridDim.x * blockDim.x) {
+        const int r = rows[i], d = dsts[i];
+        int h = -1;
+        if (r >= 0 && d >= 0 && d < V) h = hops[(size_t)r * V + d];
+        len[i] = h < 0 ? 0 : (int64_t)h + 1;
+    }
+}
+
+// block-wide exclusive scan of kScanTile values in place; block total out
+__device__ int64_t block_scan(int64_t (&v)[kScanItems], int64_t *sh)
+{
+    int64_t t = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const int64_t x = v[k];
+        v[k] = t;
+        t += x;
+    }
+    // inclusive scan of the per-thread totals across the block
+    sh[threadIdx.x] = t;
+    __syncthreads();
+    for (int o = 1; o < kScanThreads; o <<= 1) {
+        const int64_t y = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0;
+        __syncthreads();
+        sh[threadIdx.x] += y;
+        __syncthreads();
+    }
+    const int64_t excl = sh[threadIdx.x] - t;
+    const int64_t total = sh[kScanThreads - 1];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) v[k] += excl;
+    return total;
+}
+
+// phase 1: scan each tile, tile totals to sums[]
+__global__ __launch_bounds__(kScanThreads) void scan_tiles_kernel(int64_t *__restrict__ a, int64_t n,
+                                                                  int64_t *__restrict__ sums)
+{
+    __shared__ int64_t sh[kScanThreads];
+    const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+    int64_t v[kScanItems];
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) v[k] = base + k < n ? a[base + k] : 0;
+    const int64_t tot = block_scan(v, sh);
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k)
+        if (base + k < n) a[base + k] = v[k];
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// phase 2: one block scans the tile totals (any count), grand total to *total
+__global__ __launch_bounds__(kScanThreads) void scan_sums_kernel(int64_t *__restrict__ sums, int64_t n,
+                                                                 int64_t *__restrict__ total)
+{
+    __shared__ int64_t sh[kScanThreads];
+    int64_t carry = 0;
+    for (int64_t t0 = 0; t0 < n; t0 += kScanTile) {
+        const int64_t base = t0 + (int64_t)threadIdx.x * kScanItems;
+        int64_t v[kScanItems];
+#pragma unroll
+        for (int k = 0; k < kScanItems; ++k) v[k] = base + k < n ? sums[base + k] : 0;
+        const int64_t tot = block_scan(v, sh);
+#pragma unroll
+        for (int k = 0; k < kScanItems; ++k)
+            if (base + k < n) sums[base + k] = v[k] + carry;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+// phase 3: add each tile's prefix
+__global__ __launch_bounds__(256) void scan_add_kernel(int64_t *__restrict__ a, int64_t n,
+                                                       const int64_t *__restrict__ sums)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        a[i] += sums[i / kScanTile];
+}
+
+__global__ __launch_bounds__(256) void route_walk_kernel(
+    int V, const int32_t *__restrict__ parent, const int32_t *__restrict__ port,
+    const int32_t *__restrict__ rows, const int32_t *__restrict__ dsts,
+    const int32_t *__restrict__ last_port, int npairs, const int64_t *__restrict__ off,
+    int32_t *__restrict__ hop_switch, int32_t *__restrict__ hop_port)
+{
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += gridDim.x * blockDim.x) {
+        int64_t lo = off[i], j = off[i + 1] - 1;
+        if (j < lo) continue;                 // unreachable: no entries
+        const size_t rb = (size_t)rows[i] * V;
+        int x = dsts[i];
+        hop_switch[j] = x;
+        hop_port[j] = last_port[i];
+        // parent and port of x: the switch before x and its port toward x
+        while (j > lo) {
+            const int p = parent[rb + x];
+            const int pt = port[rb + x];
+            --j;
+            hop_switch[j] = p;
+            hop_port[j] = pt;
+            x = p;
+        }
+    }
+}
+
+}  // namespace
+
+int sdnr_launch_route_offsets(sdnr_ctx *ctx, const int32_t *d_hops, const int32_t *d_rows,
+                              const int32_t *d_dsts, int32_t npairs, int64_t *d_off)
+{
+    // offsets[0..npairs]: lengths into off[0..npairs), exclusive scan, the
+    // total into off[npairs]
+    const int V = ctx->V;
+    const int64_t n = npairs;
+    if (n == 0) {
+        SDNR_HIP(hipMemsetAsync(d_off, 0, sizeof(int64_t), ctx->stream));
+        return SDNR_OK;
+    }
+    const int64_t tiles = (n + kScanTile - 1) / kScanTile;
+    int rc = sdnr_reserve(&ctx->scratch, &ctx->scratch_bytes, (size_t)(tiles + 1) * 8);
+    if (rc) return rc;
+    int64_t *sums = static_cast<int64_t *>(ctx->scratch);
+    int g = (int)((n + 255) / 256);
+    if (g > ctx->num_cus * 16) g = ctx->num_cus * 16;
+    hipLaunchKernelGGL(route_len_kernel, dim3(g), dim3(256), 0, ctx->stream, V, d_hops, d_rows,
+                       d_dsts, npairs, d_off);
+    hipLaunchKernelGGL(scan_tiles_kernel, dim3((unsigned)tiles), dim3(kScanThreads), 0, ctx->stream,
+                       d_off, n, sums);
+    hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScanThreads), 0, ctx->stream, sums, tiles,
+                       d_off + n);
+    hipLaunchKernelGGL(scan_add_kernel, dim3(g), dim3(256), 0, ctx->stream, d_off, n, sums);
+    SDNR_HIP(hipGetLastError());
+    return SDNR_OK;
+}
+
+int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32_t *d_port,
+                             const int32_t *d_rows, const int32_t *d_dsts,
+                             const int32_t *d_last_port, int32_t npairs, const int64_t *d_off,
+                             int32_t *d_switch, int32_t *d_hport)
+{
+    if (npairs == 0) return SDNR_OK;
+    int g = (npairs + 255) / 256;
+    if (g > ctx->num_cus * 16) g = ctx->num_cus * 16;
+    ctx->last_kernel = "route_walk_kernel";
+    if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
+    hipLaunchKernelGGL(route_walk_kernel, dim3(g), dim3(256), 0, ctx->stream, ctx->V, d_parent,
+                       d_port, d_rows, d_dsts, d_last_port, npairs, d_off, d_switch, d_hport);
+    SDNR_HIP(hipGetLastError());
+    if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+    return SDNR_OK;
+}

@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "sdnr_abi_version", "sdnr_last_error", "sdnr_device_count", "sdnr_create",
     "sdnr_destroy", "sdnr_set_stream", "sdnr_synchronize", "sdnr_graph_upload",
     "sdnr_graph_info", "sdnr_dfs_tables", "sdnr_dfs_tables_packed", "sdnr_shortest_tables",
-    "sdnr_apsp",
+    "sdnr_apsp", "sdnr_route_offsets", "sdnr_route_expand",
     "sdnr_last_kernel_ms", "sdnr_last_kernel",
 )
 
@@ -74,6 +74,8 @@ def _bind(L):
         "sdnr_dfs_tables_packed": ([vp, vp, i32, vp, u32], c_int),
         "sdnr_shortest_tables": ([vp, vp, i32, vp, vp, vp, u32], c_int),
         "sdnr_apsp": ([vp, vp, u32], c_int),
+        "sdnr_route_offsets": ([vp, vp, i32, vp, vp, i32, vp, u32], c_int),
+        "sdnr_route_expand": ([vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp, u32], c_int),
         "sdnr_last_kernel_ms": ([vp, ctypes.POINTER(ctypes.c_float)], c_int),
         "sdnr_last_kernel": ([vp], ctypes.c_char_p),
     }
@@ -219,6 +221,41 @@ class Context(object):
         _check(self._lib.sdnr_shortest_tables(self._h, _ptr(dsts), D, _ptr(dist),
                                               _ptr(nh), _ptr(nhp), 0))
         return dist, nh, nhp
+
+    def expand_routes(self, parent, port, hops, rows, dsts, last_port):
+        """Flow entries of many pairs from host tables: (offsets int64
+        [n+1], hop_switch int32, hop_port int32); see sdnr_route_expand."""
+        parent = np.ascontiguousarray(parent, np.int32)
+        port = np.ascontiguousarray(port, np.int32)
+        hops = np.ascontiguousarray(hops, np.int32)
+        rows = np.ascontiguousarray(rows, np.int32)
+        dsts = np.ascontiguousarray(dsts, np.int32)
+        last = np.ascontiguousarray(last_port, np.int32)
+        n, nrows = int(rows.shape[0]), int(parent.shape[0])
+        off = np.empty(n + 1, np.int64)
+        _check(self._lib.sdnr_route_offsets(self._h, _ptr(hops), nrows, _ptr(rows), _ptr(dsts),
+                                            n, _ptr(off), 0))
+        total = int(off[-1])
+        sw = np.empty(total, np.int32)
+        hp = np.empty(total, np.int32)
+        _check(self._lib.sdnr_route_expand(self._h, _ptr(parent), _ptr(port), nrows, _ptr(rows),
+                                           _ptr(dsts), _ptr(last), n, _ptr(off), _ptr(sw),
+                                           _ptr(hp), 0))
+        return off, sw, hp
+
+    def route_offsets_device(self, hops_ptr, rows_ptr, dsts_ptr, npairs, off_ptr):
+        _check(self._lib.sdnr_route_offsets(self._h, ctypes.c_void_p(hops_ptr), 0,
+                                            ctypes.c_void_p(rows_ptr), ctypes.c_void_p(dsts_ptr),
+                                            int(npairs), ctypes.c_void_p(off_ptr), DEVICE_PTRS))
+
+    def expand_routes_device(self, parent_ptr, port_ptr, rows_ptr, dsts_ptr, last_ptr, npairs,
+                             off_ptr, sw_ptr, hp_ptr, timing=False):
+        flags = DEVICE_PTRS | (TIMING if timing else 0)
+        _check(self._lib.sdnr_route_expand(self._h, ctypes.c_void_p(parent_ptr),
+                                           ctypes.c_void_p(port_ptr), 0, ctypes.c_void_p(rows_ptr),
+                                           ctypes.c_void_p(dsts_ptr), ctypes.c_void_p(last_ptr),
+                                           int(npairs), ctypes.c_void_p(off_ptr),
+                                           ctypes.c_void_p(sw_ptr), ctypes.c_void_p(hp_ptr), flags))
 
     def apsp(self):
         dist = np.empty((self.V, self.V), np.uint16)

@@ -39,6 +39,12 @@ class RouteEngine(object):
         self.load(export)
         return self.ctx.shortest_tables(dsts, with_nexthop=True)
 
+    def expand(self, export, tables, rows, dsts, last_port):
+        """Flow entries of many pairs (routes.hip): (offsets, switch ids, ports)."""
+        self.load(export)
+        parent, port, hops = tables
+        return self.ctx.expand_routes(parent, port, hops, rows, dsts, last_port)
+
     def close(self):
         self.ctx.close()
 

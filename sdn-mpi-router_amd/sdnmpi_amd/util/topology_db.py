@@ -245,10 +245,53 @@ class TopologyDB(object):
                     "dpids": ex.csr.dpids}
         raise ValueError("mode must be 'dfs' or 'shortest'")
 
+    def route_entries(self, pairs):
+        """Flow entries of many (src_mac, dst_mac) pairs in one GPU pass --
+        what ``Router._add_flows_for_path`` installs for each pair (reference
+        ``sdnmpi/router.py:83-104``), e.g. for every MPI rank pair of a job.
+
+        Returns ``(offsets, dpid, port)`` numpy arrays: pair i's fdb is
+        ``list(zip(dpid[o[i]:o[i+1]], port[o[i]:o[i+1]]))``, equal to
+        ``find_route(*pairs[i])`` (empty for unknown hosts or unreachable
+        destinations).
+        """
+        pairs = list(pairs)
+        n = len(pairs)
+        ex = self.graph()
+        sv = np.full(n, -1, np.int64)
+        dv = np.full(n, -1, np.int64)
+        last = np.zeros(n, np.int64)
+        for i, (a, b) in enumerate(pairs):
+            ea, eb = self._endpoint(a), self._endpoint(b)
+            if ea is None or eb is None:
+                continue
+            sv[i] = ex.index[ea[0]]
+            dv[i] = ex.index[eb[0]]
+            last[i] = self._last_hop(eb[0], eb[1], b)[1]
+        ok = np.nonzero(sv >= 0)[0]
+        off = np.zeros(n + 1, np.int64)
+        if ok.size == 0:
+            return off, np.zeros(0, np.int64), np.zeros(0, np.int32)
+        want = sorted(set(sv[ok].tolist()))
+        batch = self._host_vertices(ex) if self._batch else ()
+        tabs = self._cache.dfs_rows(self.engine, want, batch)
+        rows = np.asarray([self._cache.dfs_row[v] for v in sv[ok].tolist()], np.int32)
+        o, sw, hp = self.engine.expand(ex, tabs, rows, dv[ok], last[ok])
+        lens = np.zeros(n, np.int64)
+        lens[ok] = np.diff(o)
+        np.cumsum(lens, out=off[1:])
+        return off, ex.csr.dpids[sw], hp
+
     def find_routes(self, pairs, multiple=False):
         """find_route over many (src_mac, dst_mac) pairs; tables are computed
-        once for all of them."""
+        once for all of them, and the default-route fdbs of large batches are
+        expanded on the GPU (``route_entries``)."""
         pairs = list(pairs)
+        if not multiple and len(pairs) >= 64:
+            off, dp, pt = self.route_entries(pairs)
+            dp, pt = dp.tolist(), pt.tolist()
+            o = off.tolist()
+            return [list(zip(dp[o[i]:o[i + 1]], pt[o[i]:o[i + 1]])) for i in range(len(pairs))]
         if not multiple and self._batch:
             ex = self.graph()
             want = set()

@@ -156,6 +156,16 @@ class _FakeEngine(object):
         self.calls.append(("sp", export.key, tuple(int(x) for x in dsts)))
         return self.O.dest_tables(export.csr, dsts)
 
+    def expand(self, export, tables, rows, dsts, last_port):
+        # numpy restatement of routes.hip (test double only)
+        from sdnmpi_amd.engine import expand_tree_paths
+        parent, port, _ = tables
+        off, verts, ports = expand_tree_paths(parent, port, rows, dsts)
+        ends = off[1:] - 1
+        ok = off[1:] > off[:-1]
+        ports[ends[ok]] = np.asarray(last_port)[ok]
+        return off, verts.astype(np.int32), ports.astype(np.int32)
+
 
 def test_dict_mutations_invalidate_tables():
     eng = _FakeEngine()
@@ -257,3 +267,43 @@ def test_link_failure_incremental_gpu():
     from sdnmpi_amd import topologies as T
     fabric = T.fat_tree(8)
     _link_failure_replay(fabric.populate(TopologyDB()), fabric)
+
+
+def test_route_entries_batched_fake_engine():
+    from oracle import oracle as O
+    from sdnmpi_amd import topologies as T
+    fabric = T.fat_tree(4)
+    db = fabric.populate(TopologyDB())
+    db._engine = _FakeEngine()
+    macs = fabric.host_macs() + ["00:00:00:00:00:05", "02:00:00:00:00:77"]   # local, unknown
+    pairs = [(a, b) for a in macs for b in macs]
+    got = db.find_routes(pairs)
+    assert got == [O.find_route_pair(db, a, b) for a, b in pairs]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["mock", "fat_tree_k8", "dragonfly_a4_h2_p2", "random_V40",
+                                  "torus_5x3x2"])
+def test_route_entries_match_reference(name):
+    """GPU flow-entry emission for every host pair (plus switch-local and
+    unknown MACs) equals the reference's fdb lists."""
+    from oracle import oracle as O
+    g = G.Golden(name)
+    fabric = g.fabric()
+    db = fabric.populate(TopologyDB())
+    macs = fabric.host_macs()
+    got = db.find_routes([(macs[int(a)], macs[int(b)]) for a, b in zip(g.pair_src, g.pair_dst)])
+    assert got == [g.fdb(i) for i in range(len(g))]
+    extra = macs[:3] + ["00:00:00:00:00:01", "02:00:00:00:00:77"]
+    pairs = [(a, b) for a in extra for b in macs[-20:] + extra] * 4
+    assert db.find_routes(pairs) == [O.find_route_pair(db, a, b) for a, b in pairs]
+
+
+@pytest.mark.gpu
+def test_route_entries_k48_golden_pairs():
+    g = G.Golden("fat_tree_k48_sample")
+    fabric = g.fabric()
+    db = fabric.populate(TopologyDB())
+    macs = fabric.host_macs()
+    got = db.find_routes([(macs[int(a)], macs[int(b)]) for a, b in zip(g.pair_src, g.pair_dst)])
+    assert got == [g.fdb(i) for i in range(len(g))]
