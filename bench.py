@@ -241,8 +241,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BENCH_DEVICE pins every rank to one device (rehearsing the N > 1 code
+    # path on a one-GPU box); the driver never sets it
+    if os.environ.get("BENCH_DEVICE"):
+        local = int(os.environ["BENCH_DEVICE"])
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")   # gloo: rehearsal only
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if args.mode == "flows":
@@ -269,37 +277,56 @@ def main():
         csr.E > 0 and int(csr.port.min()) >= 0 and int(csr.port.max()) < 0xFFFF
     if args.layout == "packed" and not packed:
         raise SystemExit("--layout packed: fabric has V > 65535 or ports >= 0xFFFF")
-    if packed:
-        a = torch.empty((per, V), dtype=torch.int32, device=dev)     # parent | port << 16
-        b = c = None
-    elif args.mode == "dfs":
-        a = torch.empty((per, V), dtype=torch.int32, device=dev)     # parent
-        b = torch.empty((per, V), dtype=torch.int32, device=dev)     # port
-        c = None
-    else:
-        a = torch.empty((per, V), dtype=torch.int16, device=dev)     # dist (u16)
-        b = torch.empty((per, V), dtype=torch.int32, device=dev)     # nh
-        c = torch.empty((per, V), dtype=torch.int32, device=dev)     # nh_port
+    def tables():
+        if packed:
+            return (torch.empty((per, V), dtype=torch.int32, device=dev),)   # parent | port << 16
+        if args.mode == "dfs":
+            return (torch.empty((per, V), dtype=torch.int32, device=dev),    # parent
+                    torch.empty((per, V), dtype=torch.int32, device=dev))    # port
+        return (torch.empty((per, V), dtype=torch.int16, device=dev),        # dist (u16)
+                torch.empty((per, V), dtype=torch.int32, device=dev),        # nh
+                torch.empty((per, V), dtype=torch.int32, device=dev))        # nh_port
+
+    # N > 1: two table sets, so step i+1's kernel (our stream) overlaps step
+    # i's all-gather (RCCL's stream); a set is reused only after its gather
+    nbuf = 2 if world > 1 else 1
+    bufs = [tables() for _ in range(nbuf)]
+    gathered = [tuple(torch.empty((world * per, V), dtype=t.dtype, device=dev) for t in b)
+                for b in bufs]
+    pending = [[] for _ in range(nbuf)]
+    counter = [0]
 
     def step(ev=None):
+        k = counter[0] % nbuf
+        counter[0] += 1
+        for w in pending[k]:                # this set's previous gather is done
+            w.wait()
+        pending[k] = []
+        tb = bufs[k]
         if ev is not None:
             ev[0].record(stream)
         if packed:
-            ctx.dfs_tables_packed_device(t_src.data_ptr(), per, a.data_ptr())
+            ctx.dfs_tables_packed_device(t_src.data_ptr(), per, tb[0].data_ptr())
         elif args.mode == "dfs":
-            ctx.dfs_tables_device(t_src.data_ptr(), per, a.data_ptr(), b.data_ptr())
+            ctx.dfs_tables_device(t_src.data_ptr(), per, tb[0].data_ptr(), tb[1].data_ptr())
         else:
-            ctx.shortest_tables_device(t_src.data_ptr(), per, a.data_ptr(), b.data_ptr(),
-                                       c.data_ptr())
+            ctx.shortest_tables_device(t_src.data_ptr(), per, tb[0].data_ptr(), tb[1].data_ptr(),
+                                       tb[2].data_ptr())
         if ev is not None:
             ev[1].record(stream)
         if world > 1:                       # assemble [sources][V] on every rank
-            for t in (a, b, c):
-                if t is not None:
-                    D.all_gather_rows(t)
+            for t, g in zip(tb, gathered[k]):
+                pending[k].append(D.all_gather_rows_async(t, g))
+
+    def drain():
+        for k in range(nbuf):
+            for w in pending[k]:
+                w.wait()
+            pending[k] = []
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize(dev)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
@@ -309,6 +336,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(evs[i])
+    drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -353,7 +381,8 @@ def main():
             "fabric": args.fabric, "V": V, "E": E, "hosts": H, "sources": S,
             "host_pairs_per_step": int(routes), "table_layout": layout,
             "parallelism": "sources sharded over %d GPU(s)%s" % (
-                world, " + RCCL all-gather" if world > 1 else ""),
+                world, " + RCCL all-gather of the tables (double-buffered: step i+1's "
+                       "kernel overlaps step i's gather)" if world > 1 else ""),
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

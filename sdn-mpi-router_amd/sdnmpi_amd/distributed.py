@@ -14,7 +14,7 @@ into an all-(-1) row; ``unpad`` drops it after the gather.
 import torch
 import torch.distributed as dist
 
-__all__ = ["shard_bounds", "padded_shard", "all_gather_rows", "unpad"]
+__all__ = ["shard_bounds", "padded_shard", "all_gather_rows", "all_gather_rows_async", "unpad"]
 
 
 def shard_bounds(n, world, rank):
@@ -51,6 +51,33 @@ def all_gather_rows(local, group=None):
         parts = list(out.chunk(world, 0))
         dist.all_gather(parts, local.contiguous(), group=group)
     return out
+
+
+def all_gather_rows_async(local, out, group=None):
+    """Asynchronous all-gather of [per, V] rows into ``out`` [world*per, V]
+    (rank order); returns the work handle.  On the nccl backend it runs on
+    RCCL's stream, after the work already queued on the current stream, so
+    the next kernel launched on the current stream overlaps it; ``wait()``
+    before ``local`` or ``out`` is reused."""
+    if dist.get_backend(group) == "nccl":
+        return dist.all_gather_into_tensor(out, local.contiguous(), group=group, async_op=True)
+    if local.is_cuda:        # gloo with device tensors (rehearsal): through host memory
+        host = torch.empty(out.shape, dtype=out.dtype)
+        src = local.contiguous().cpu()
+        if src.dtype == torch.int16:         # gloo has no 16-bit integers: move bytes
+            src, hv = src.view(torch.uint8), host.view(torch.uint8)
+        else:
+            hv = host
+        dist.all_gather(list(hv.chunk(dist.get_world_size(group), 0)), src, group=group)
+        out.copy_(host)
+        return _Done()
+    parts = list(out.chunk(dist.get_world_size(group), 0))
+    return dist.all_gather(parts, local.contiguous(), group=group, async_op=True)
+
+
+class _Done(object):
+    def wait(self):
+        return True
 
 
 def unpad(table, n):

@@ -41,7 +41,10 @@ def _worker(rank, world, port, fabric_name, q):
             p, t, _ = O.dfs_tables(csr, mine[ok], with_hops=False, nthreads=1)
             parent[ok], port[ok] = p, t
         gp = D.unpad(D.all_gather_rows(torch.from_numpy(parent)), len(srcs))
-        gt = D.unpad(D.all_gather_rows(torch.from_numpy(port)), len(srcs))
+        # the bench's double-buffered form: async gathers into preallocated outputs
+        out = torch.empty((world * len(mine), csr.V), dtype=torch.int32)
+        D.all_gather_rows_async(torch.from_numpy(port), out).wait()
+        gt = D.unpad(out, len(srcs))
         if rank == 0:
             po, to, _ = O.dfs_tables(csr, srcs, with_hops=False, nthreads=1)
             q.put(bool(np.array_equal(gp.numpy(), po) and np.array_equal(gt.numpy(), to)))
