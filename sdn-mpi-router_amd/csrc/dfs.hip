@@ -900,7 +900,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_count_kernel(
 // ballots per pop than one-row-per-wavefront.  Same exact semantics as
 // dfs_global_batch_kernel (first live entry from the top is processed).
 // ---------------------------------------------------------------------------
-template <int LPR, int J, bool HOPS>
+template <int LPR, int J, bool HOPS, int RING>
 __global__ __launch_bounds__(64) void dfs_global_packed_kernel(
     int V, int W, const int32_t *__restrict__ col, const int32_t *__restrict__ port,
     const int32_t *__restrict__ src, int nsrc, int32_t *__restrict__ out_parent,
@@ -949,16 +949,16 @@ __global__ __launch_bounds__(64) void dfs_global_packed_kernel(
         for (;;) {
             if (lsp == 0) {
                 if (gsp == 0) break;
-                const int n = gsp < kRing / 2 ? gsp : kRing / 2;
+                const int n = gsp < RING / 2 ? gsp : RING / 2;
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                bot = (bot - n) & (kRing - 1);
+                bot = (bot - n) & (RING - 1);
                 for (int i = lane; i < n; i += SDNR_WAVE)
-                    ring[(bot + i) & (kRing - 1)] = spill[gsp - n + i];
+                    ring[(bot + i) & (RING - 1)] = spill[gsp - n + i];
                 gsp -= n;
                 lsp = n;
             }
             const int kk = lsp < K ? lsp : K;
-            uint2 me = ring[(bot + lsp - 1 - lane) & (kRing - 1)];
+            uint2 me = ring[(bot + lsp - 1 - lane) & (RING - 1)];
             me.x = lane < kk ? me.x : 0u;
             me.y = lane < kk ? me.y : 0u;
             int x[J];
@@ -1003,12 +1003,12 @@ __global__ __launch_bounds__(64) void dfs_global_packed_kernel(
             const uint32_t ed = (uint32_t)read_lane((int)me.y, istar);
             lsp -= istar + 1;
             const int cnt = __popcll(mm);
-            if (lsp + cnt > kRing) {
-                for (int i = lane; i < kRing / 2; i += SDNR_WAVE)
-                    spill[gsp + i] = ring[(bot + i) & (kRing - 1)];
-                gsp += kRing / 2;
-                bot = (bot + kRing / 2) & (kRing - 1);
-                lsp -= kRing / 2;
+            if (lsp + cnt > RING) {
+                for (int i = lane; i < RING / 2; i += SDNR_WAVE)
+                    spill[gsp + i] = ring[(bot + i) & (RING - 1)];
+                gsp += RING / 2;
+                bot = (bot + RING / 2) & (RING - 1);
+                lsp -= RING / 2;
             }
             if ((mm >> lane) & 1ull) {
                 const int rank = lanes_below(mm);
@@ -1016,7 +1016,7 @@ __global__ __launch_bounds__(64) void dfs_global_packed_kernel(
                 prow[vv] = eu;
                 trow[vv] = port[eu * W + pos];
                 if (HOPS) hrow[vv] = (int)ed + 1;
-                ring[(bot + lsp + rank) & (kRing - 1)] = make_uint2((uint32_t)vv, ed + 1u);
+                ring[(bot + lsp + rank) & (RING - 1)] = make_uint2((uint32_t)vv, ed + 1u);
             }
             lsp += cnt;
         }
@@ -1370,10 +1370,37 @@ static size_t dfs_lds_bytes_small(int V)
     return align16(4 * VWp + 8 * (size_t)V + 2 * (size_t)V);
 }
 
-static size_t dfs_lds_bytes_global(int V)
+static size_t dfs_lds_bytes_global(int V, int ring = kRing)
 {
     const size_t VWp = (size_t)((((V + 31) >> 5) + 3) & ~3);
-    return align16(4 * VWp + 8 * (size_t)kRing);
+    return align16(4 * VWp + 8 * (size_t)ring);
+}
+
+// stack-ring entries of the lane-packed kernel: small rings leave room for
+// more resident sources on large graphs (the torus search is a chain of
+// ~14k non-leaf pops per source: throughput comes from sources in flight);
+// SDNROUTE_DFS_RING=128|1024 overrides
+static int packed_ring(int V, int W)
+{
+    if (const char *f = getenv("SDNROUTE_DFS_RING")) {
+        const int r = atoi(f);
+        if (r == 128 || r == 1024) return r;
+    }
+    return V > 16384 && W <= 8 ? 128 : 1024;
+}
+
+// stack entries checked per batch by the lane-packed kernel with 8 lanes per
+// row: J = 1 (8 entries) or 2 (16).  On the torus 13.6k of 32.8k pops push
+// children, so a batch rarely retires more than two entries: the narrower
+// batch halves the row traffic per step (torus 32^3: 108 -> 99 ms).
+// SDNROUTE_DFS_PACKED_J overrides
+static int packed_j8(int V)
+{
+    if (const char *f = getenv("SDNROUTE_DFS_PACKED_J")) {
+        const int j = atoi(f);
+        if (j == 1 || j == 2) return j;
+    }
+    return V > 16384 ? 1 : 2;
 }
 
 namespace {
@@ -1680,22 +1707,43 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
     } else if (!small && ell && ctx->W <= 32 && packed_ok()) {
         // lanes per row = next power of two >= W
         const int lpr = ctx->W <= 8 ? 8 : (ctx->W <= 16 ? 16 : 32);
-        ctx->last_kernel = "dfs_global_packed_kernel";
-#define SDNR_PACKED(L_, J_, H_)                                                              \
+        const int ring = packed_ring(V, ctx->W);
+        const size_t plds = dfs_lds_bytes_global(V, ring);
+        size_t pbpc = SDNR_LDS_PER_CU / plds;
+        if (pbpc > 32) pbpc = 32;                // 32 one-wave blocks fill a CU
+        if (pbpc < 1) pbpc = 1;
+        int pgrid = (int)((size_t)ctx->num_cus * pbpc);
+        if (pgrid > nsrc) pgrid = nsrc;
+        if (pgrid > grid) {                      // spill area: V entries per block
+            int rc = sdnr_reserve(&ctx->scratch, &ctx->scratch_bytes,
+                                  (size_t)pgrid * (size_t)V * sizeof(uint2));
+            if (rc) return rc;
+            spill = static_cast<uint2 *>(ctx->scratch);
+        }
+        ctx->last_kernel = ring == 128 ? "dfs_global_packed_kernel<ring128>"
+                                       : "dfs_global_packed_kernel";
+#define SDNR_PACKED(L_, J_, H_, R_)                                                          \
     do {                                                                                     \
-        auto k = dfs_global_packed_kernel<L_, J_, H_>;                                       \
+        auto k = dfs_global_packed_kernel<L_, J_, H_, R_>;                                   \
         allow_full_lds(k);                                                                   \
-        hipLaunchKernelGGL(k, dim3(grid), dim3(64), lds, ctx->stream, V, ctx->W,             \
+        hipLaunchKernelGGL(k, dim3(pgrid), dim3(64), plds, ctx->stream, V, ctx->W,           \
                            ctx->ell_col, ctx->ell_port, d_src, nsrc, d_parent, d_port,       \
                            d_hops, spill);                                                   \
     } while (0)
-        if (lpr == 8) {
-            if (hops) SDNR_PACKED(8, 2, true); else SDNR_PACKED(8, 2, false);
+#define SDNR_PACKED_R(L_, J_, H_)                                                            \
+    do {                                                                                     \
+        if (ring == 128) SDNR_PACKED(L_, J_, H_, 128); else SDNR_PACKED(L_, J_, H_, 1024);   \
+    } while (0)
+        if (lpr == 8 && packed_j8(V) == 1) {
+            if (hops) SDNR_PACKED_R(8, 1, true); else SDNR_PACKED_R(8, 1, false);
+        } else if (lpr == 8) {
+            if (hops) SDNR_PACKED_R(8, 2, true); else SDNR_PACKED_R(8, 2, false);
         } else if (lpr == 16) {
-            if (hops) SDNR_PACKED(16, 4, true); else SDNR_PACKED(16, 4, false);
+            if (hops) SDNR_PACKED_R(16, 4, true); else SDNR_PACKED_R(16, 4, false);
         } else {
-            if (hops) SDNR_PACKED(32, 8, true); else SDNR_PACKED(32, 8, false);
+            if (hops) SDNR_PACKED_R(32, 8, true); else SDNR_PACKED_R(32, 8, false);
         }
+#undef SDNR_PACKED_R
 #undef SDNR_PACKED
     } else if (narrow) {
         const int K = dfs_batch_depth(ctx);

@@ -29,6 +29,9 @@ def ctx():
 
 
 def _strategy(monkeypatch, dfs=None, ell=None):
+    if dfs == "global-ring128":
+        monkeypatch.setenv("SDNROUTE_DFS_RING", "128")
+        dfs = "global"
     if dfs == "global-nopack":
         monkeypatch.setenv("SDNROUTE_DFS_PACKED", "0")
         dfs = "global"
@@ -60,7 +63,8 @@ def _check_pairs(g, fabric, p, t, srcs):
         assert got == g.fdb(i), (g.name, i)
 
 
-@pytest.mark.parametrize("strategy", ["auto", "async", "count", "coop", "lds", "global", "global-nopack"])
+@pytest.mark.parametrize("strategy", ["auto", "async", "count", "coop", "lds", "global",
+                                      "global-ring128", "global-nopack"])
 @pytest.mark.parametrize("ell", [True, False])
 @pytest.mark.parametrize("name", G.SMALL)
 def test_dfs_small_all_sources(ctx, monkeypatch, name, strategy, ell):
