@@ -178,7 +178,7 @@ def main_flows(args, world, rank, local, dev):
     def step(timing=False):
         ctx.route_offsets_device(hop.data_ptr(), t_rows.data_ptr(), t_dsts.data_ptr(), n,
                                  off.data_ptr())
-        ctx.expand_routes_device(par.data_ptr(), prt.data_ptr(), t_rows.data_ptr(),
+        ctx.expand_routes_device(par.data_ptr(), prt.data_ptr(), S, t_rows.data_ptr(),
                                  t_dsts.data_ptr(), t_last.data_ptr(), n, off.data_ptr(),
                                  sw.data_ptr(), hpo.data_ptr(), timing=timing)
 
@@ -203,7 +203,7 @@ def main_flows(args, world, rank, local, dev):
         elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3
     kern_ms = float(np.mean(kms))
-    # walk kernel: per entry parent + port read (8 B) and (switch, port)
+    # expansion: per entry parent + port read (8 B) and (switch, port)
     # written (8 B); per pair row/dst/last_port (12 B) + offsets pair (16 B)
     bytes_launch = 16 * total + 28 * n
     achieved = bytes_launch / (kern_ms / 1e3) / 1e9
@@ -225,7 +225,7 @@ def main_flows(args, world, rank, local, dev):
             "parallelism": "pairs sharded over %d GPU(s)" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "route_walk_kernel", "kernel_ms": kern_ms,
+                     "kernel": ctx.last_kernel(), "kernel_ms": kern_ms,
                      "bytes_per_launch": bytes_launch},
         "entries_per_s": float(total) * world / (ms / 1e3),
     }

@@ -143,7 +143,9 @@ int sdnr_apsp(sdnr_ctx *ctx, uint16_t *dist, uint32_t flags);
  *   order: hop_switch[j] = dense switch id, hop_port[j] = its out port; the
  *   last entry is (dsts[i], last_port[i]).  Bit-identical to find_route's
  *   fdb with switch ids mapped to dpids.
- * Host buffers: the tables are staged per call (nrows * V entries each). */
+ * nrows is required in both modes (the expansion builds an 8th-ancestor
+ * table of the nrows trees).  Host buffers: the tables are staged per call
+ * (nrows * V entries each). */
 int sdnr_route_offsets(sdnr_ctx *ctx, const int32_t *hops, int32_t nrows,
                        const int32_t *rows, const int32_t *dsts, int32_t npairs,
                        int64_t *offsets, uint32_t flags);

@@ -487,8 +487,8 @@ int sdnr_route_expand(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port,
         (npairs > 0 && (!parent || !port || !rows || !dsts || !last_port)))
         return sdnr_fail(SDNR_ERR_INVAL, "sdnr_route_expand: bad arguments");
     if (flags & SDNR_DEVICE_PTRS)
-        return sdnr_launch_route_expand(ctx, parent, port, rows, dsts, last_port, npairs, offsets,
-                                        hop_switch, hop_port);
+        return sdnr_launch_route_expand(ctx, parent, port, nrows, rows, dsts, last_port, npairs,
+                                        offsets, hop_switch, hop_port);
     if ((rc = check_pairs(ctx, nrows, rows, dsts, npairs, "sdnr_route_expand"))) return rc;
     const int64_t total = offsets[npairs];
     if (total > 0 && (!hop_switch || !hop_port))
@@ -517,7 +517,7 @@ int sdnr_route_expand(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port,
     SDNR_HIP(hipMemcpyAsync(d_l, last_port, pr, hipMemcpyHostToDevice, ctx->stream));
     SDNR_HIP(hipMemcpyAsync(d_o, offsets, ((size_t)npairs + 1) * 8, hipMemcpyHostToDevice,
                             ctx->stream));
-    if ((rc = sdnr_launch_route_expand(ctx, d_p, d_t, d_r, d_d, d_l, npairs, d_o, d_s, d_q)))
+    if ((rc = sdnr_launch_route_expand(ctx, d_p, d_t, nrows, d_r, d_d, d_l, npairs, d_o, d_s, d_q)))
         return rc;
     if (ent) {
         SDNR_HIP(hipMemcpyAsync(hop_switch, d_s, ent, hipMemcpyDeviceToHost, ctx->stream));

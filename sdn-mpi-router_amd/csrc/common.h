@@ -105,6 +105,6 @@ int sdnr_launch_apsp(sdnr_ctx *ctx, uint16_t *d_dist);
 int sdnr_launch_route_offsets(sdnr_ctx *ctx, const int32_t *d_hops, const int32_t *d_rows,
                               const int32_t *d_dsts, int32_t npairs, int64_t *d_off);
 int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32_t *d_port,
-                             const int32_t *d_rows, const int32_t *d_dsts,
+                             int32_t nrows, const int32_t *d_rows, const int32_t *d_dsts,
                              const int32_t *d_last_port, int32_t npairs, const int64_t *d_off,
                              int32_t *d_switch, int32_t *d_hport);

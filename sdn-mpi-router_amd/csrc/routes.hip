@@ -11,9 +11,17 @@
 //   offsets[i] .. offsets[i+1]   entries of pair i (0 if unreachable),
 //   hop_switch[j], hop_port[j]   dense switch id and out port of entry j.
 // Pass 1 (route_len_kernel + a three-phase scan) sizes every pair from the
-// hop table; pass 2 (route_walk_kernel) walks each pair's tree path from the
-// destination up, writing entries back to front.  The tree rows stay L2 /
-// Infinity-Cache resident; the output is written once, in order.
+// hop table; pass 2 walks each pair's tree path from the destination up,
+// writing entries back to front: route_jump_kernel<16> splits every walk over
+// 16 lanes with a 16th-ancestor table (four compositions of the parent
+// table), so the lanes of a pair store 16 consecutive entries per step and a
+// path of h hops costs ~k + h/16 dependent loads (k < 16: the lane's start);
+// route_walk_kernel (one lane per pair, SDNROUTE_ROUTE_WALK=serial) is the
+// plain form.  The tree rows stay L2 / Infinity-Cache resident; the output is
+// written once.
+#include <stdlib.h>
+#include <string.h>
+
 #include "common.h"
 
 namespace {
@@ -106,6 +114,58 @@ __global__ __launch_bounds__(256) void scan_add_kernel(int64_t *__restrict__ a, 
         a[i] += sums[i / kScanTile];
 }
 
+// anc_out[r][v] = a[r][b[r][v]] (-1 stays -1): composing the parent table
+// with itself by doubling gives the 2^j-th ancestor table of every tree
+__global__ __launch_bounds__(256) void tree_compose_kernel(int V, size_t n,
+                                                           const int32_t *__restrict__ a,
+                                                           const int32_t *__restrict__ b,
+                                                           int32_t *__restrict__ out)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const int32_t x = b[i];
+        out[i] = x < 0 ? -1 : a[(i / (size_t)V) * V + x];
+    }
+}
+
+// P lanes per pair: lane k starts at the k-th ancestor of the destination
+// (k parent steps) and then jumps P ancestors at a time, writing the entry of
+// each ancestor's parent.  The P lanes of a pair write P consecutive entries
+// per step (one 4*P-byte segment per output array instead of P scattered
+// words), and a path of h hops takes about k + h/P dependent loads instead of
+// h.
+template <int P>
+__global__ __launch_bounds__(256) void route_jump_kernel(
+    int V, const int32_t *__restrict__ parent, const int32_t *__restrict__ port,
+    const int32_t *__restrict__ ancP, const int32_t *__restrict__ rows,
+    const int32_t *__restrict__ dsts, const int32_t *__restrict__ last_port, int npairs,
+    const int64_t *__restrict__ off, int32_t *__restrict__ hop_switch,
+    int32_t *__restrict__ hop_port)
+{
+    const int64_t nthr = (int64_t)npairs * P;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nthr;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int i = (int)(t / P), k = (int)(t % P);
+        const int64_t lo = off[i], hi = off[i + 1];
+        if (hi <= lo) continue;               // unreachable: no entries
+        const int64_t h = hi - lo - 1;        // hops; entry h is the destination
+        const size_t rb = (size_t)rows[i] * V;
+        int y = dsts[i];
+        if (k == 0) {
+            hop_switch[lo + h] = y;
+            hop_port[lo + h] = last_port[i];
+        }
+        for (int s = 0; s < k && s < h; ++s) y = parent[rb + y];
+        // y = x_u, the ancestor u steps above the destination: its parent's
+        // entry (switch, port toward y) goes to index h - u - 1
+        for (int64_t u = k; u < h; u += P) {
+            hop_switch[lo + h - u - 1] = parent[rb + y];
+            hop_port[lo + h - u - 1] = port[rb + y];
+            if (u + P < h) y = ancP[rb + y];
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void route_walk_kernel(
     int V, const int32_t *__restrict__ parent, const int32_t *__restrict__ port,
     const int32_t *__restrict__ rows, const int32_t *__restrict__ dsts,
@@ -162,17 +222,62 @@ int sdnr_launch_route_offsets(sdnr_ctx *ctx, const int32_t *d_hops, const int32_
 }
 
 int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32_t *d_port,
-                             const int32_t *d_rows, const int32_t *d_dsts,
+                             int32_t nrows, const int32_t *d_rows, const int32_t *d_dsts,
                              const int32_t *d_last_port, int32_t npairs, const int64_t *d_off,
                              int32_t *d_switch, int32_t *d_hport)
 {
     if (npairs == 0) return SDNR_OK;
-    int g = (npairs + 255) / 256;
-    if (g > ctx->num_cus * 16) g = ctx->num_cus * 16;
-    ctx->last_kernel = "route_walk_kernel";
+    const char *f = getenv("SDNROUTE_ROUTE_WALK");      // "serial": one lane per pair
+    const bool serial = f && !strcmp(f, "serial");
+    const size_t n = (size_t)nrows * (size_t)ctx->V;
+    int32_t *anc = nullptr, *tmp = nullptr;
+    if (!serial) {
+        int rc = sdnr_reserve(&ctx->scratch2, &ctx->scratch2_bytes, 2 * n * sizeof(int32_t) + 64);
+        if (rc) return rc;
+        anc = static_cast<int32_t *>(ctx->scratch2);
+        tmp = anc + n;
+    }
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
-    hipLaunchKernelGGL(route_walk_kernel, dim3(g), dim3(256), 0, ctx->stream, ctx->V, d_parent,
-                       d_port, d_rows, d_dsts, d_last_port, npairs, d_off, d_switch, d_hport);
+    if (serial) {
+        int g = (npairs + 255) / 256;
+        if (g > ctx->num_cus * 16) g = ctx->num_cus * 16;
+        ctx->last_kernel = "route_walk_kernel";
+        hipLaunchKernelGGL(route_walk_kernel, dim3(g), dim3(256), 0, ctx->stream, ctx->V, d_parent,
+                           d_port, d_rows, d_dsts, d_last_port, npairs, d_off, d_switch, d_hport);
+    } else {
+        // P-th ancestors by doubling: p2 = p o p, p4 = p2 o p2, ...
+        // SDNROUTE_ROUTE_P=4|8|16 lanes per pair (default 16: k=48 1M rank
+        // pairs 0.57 ms at 8, 0.54 ms at 16, 0.75 ms at 4)
+        const char *pf = getenv("SDNROUTE_ROUTE_P");
+        const int P = pf && (atoi(pf) == 4 || atoi(pf) == 8) ? atoi(pf) : 16;
+        const int cg = ctx->num_cus * 8;
+        const int32_t *cur = d_parent;
+        int32_t *bufs[2] = {tmp, anc};
+        int which = 0;
+        for (int q = 1; q < P; q <<= 1) {
+            hipLaunchKernelGGL(tree_compose_kernel, dim3(cg), dim3(256), 0, ctx->stream, ctx->V,
+                               n, cur, cur, bufs[which]);
+            cur = bufs[which];
+            which ^= 1;
+        }
+        int64_t g = ((int64_t)npairs * P + 255) / 256;
+        if (g > ctx->num_cus * 16) g = ctx->num_cus * 16;
+#define SDNR_JUMP(P_)                                                                        \
+    hipLaunchKernelGGL(route_jump_kernel<P_>, dim3((unsigned)g), dim3(256), 0, ctx->stream,  \
+                       ctx->V, d_parent, d_port, cur, d_rows, d_dsts, d_last_port, npairs,   \
+                       d_off, d_switch, d_hport)
+        if (P == 4) {
+            ctx->last_kernel = "route_jump_kernel<4>";
+            SDNR_JUMP(4);
+        } else if (P == 8) {
+            ctx->last_kernel = "route_jump_kernel<8>";
+            SDNR_JUMP(8);
+        } else {
+            ctx->last_kernel = "route_jump_kernel<16>";
+            SDNR_JUMP(16);
+        }
+#undef SDNR_JUMP
+    }
     SDNR_HIP(hipGetLastError());
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
     return SDNR_OK;

@@ -248,11 +248,12 @@ class Context(object):
                                             ctypes.c_void_p(rows_ptr), ctypes.c_void_p(dsts_ptr),
                                             int(npairs), ctypes.c_void_p(off_ptr), DEVICE_PTRS))
 
-    def expand_routes_device(self, parent_ptr, port_ptr, rows_ptr, dsts_ptr, last_ptr, npairs,
-                             off_ptr, sw_ptr, hp_ptr, timing=False):
+    def expand_routes_device(self, parent_ptr, port_ptr, nrows, rows_ptr, dsts_ptr, last_ptr,
+                             npairs, off_ptr, sw_ptr, hp_ptr, timing=False):
         flags = DEVICE_PTRS | (TIMING if timing else 0)
         _check(self._lib.sdnr_route_expand(self._h, ctypes.c_void_p(parent_ptr),
-                                           ctypes.c_void_p(port_ptr), 0, ctypes.c_void_p(rows_ptr),
+                                           ctypes.c_void_p(port_ptr), int(nrows),
+                                           ctypes.c_void_p(rows_ptr),
                                            ctypes.c_void_p(dsts_ptr), ctypes.c_void_p(last_ptr),
                                            int(npairs), ctypes.c_void_p(off_ptr),
                                            ctypes.c_void_p(sw_ptr), ctypes.c_void_p(hp_ptr), flags))

@@ -282,12 +282,17 @@ def test_route_entries_batched_fake_engine():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("walk", ["auto", "serial", "p4", "p8"])
 @pytest.mark.parametrize("name", ["mock", "fat_tree_k8", "dragonfly_a4_h2_p2", "random_V40",
                                   "torus_5x3x2"])
-def test_route_entries_match_reference(name):
+def test_route_entries_match_reference(monkeypatch, name, walk):
     """GPU flow-entry emission for every host pair (plus switch-local and
     unknown MACs) equals the reference's fdb lists."""
     from oracle import oracle as O
+    if walk == "serial":
+        monkeypatch.setenv("SDNROUTE_ROUTE_WALK", walk)
+    elif walk != "auto":
+        monkeypatch.setenv("SDNROUTE_ROUTE_P", walk[1:])
     g = G.Golden(name)
     fabric = g.fabric()
     db = fabric.populate(TopologyDB())
