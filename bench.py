@@ -393,6 +393,21 @@ def main():
         "switch_pair_routes_per_s": float(S) * V / (ms_per_step / 1e3),
         "teps": float(hi - lo) * E / (kern_ms / 1e3),
     }
+    if rank == 0 and world == 1 and args.mode == "dfs":
+        # the drop-in's host-buffer boundary: sources in, tables out over PCIe
+        ctx.set_stream(None)
+        reps = max(1, min(5, args.steps))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            if packed:
+                ctx.dfs_tables_packed(srcs)
+            else:
+                ctx.dfs_tables(srcs, with_hops=False)
+        dt = (time.perf_counter() - t0) / reps
+        out["host_boundary"] = {
+            "value": routes / dt, "unit": "routes/s", "ms_per_call": dt * 1e3,
+            "note": "sdnr_dfs_tables%s with host buffers (sources H2D, tables D2H, "
+                    "synchronous), not the HBM-resident bench value" % ("_packed" if packed else "")}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "dfs":
         base, ref = cpu_baseline(fabric, csr, srcs, counts, H, args.cpu_budget_s)
         out["cpu_baseline"] = base
