@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--fabric", default="fat_tree:48")
-    ap.add_argument("--mode", choices=["dfs", "shortest", "flows"], default="dfs")
+    ap.add_argument("--mode", choices=["dfs", "shortest", "flows", "ecmp"], default="dfs")
     ap.add_argument("--ranks", type=int, default=1024,
                     help="flows mode: MPI ranks placed on random hosts; every ordered "
                          "rank pair's flow entries are emitted per step")
@@ -236,6 +236,72 @@ def main_flows(args, world, rank, local, dev):
         dist.destroy_process_group()
 
 
+def main_ecmp(args, world, rank, local, dev):
+    """ECMP-set sizes: the number of shortest routes of
+    every host-switch pair, the count find_route(..., multiple=True) returns
+    (reference topology_db.py:86-122, exponential there), by a level DP over
+    the shortest-path DAG per destination.  Distances resident in HBM; one
+    step = the counts of all destinations; value = switch pairs per second."""
+    fabric = T.by_name(args.fabric)
+    csr = fabric.csr()
+    V = csr.V
+    dsts = np.unique(fabric.host_table()[0]).astype(np.int32)
+    lo, hi, per = D.shard_bounds(len(dsts), world, rank)
+    my = D.padded_shard(dsts, world, rank)
+    ctx = _native.Context(local)
+    ctx.upload(csr)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream.cuda_stream)
+    t_dst = my.to(dev)
+    dist_t = torch.empty((per, V), dtype=torch.int16, device=dev)
+    ctx.shortest_tables_device(t_dst.data_ptr(), per, dist_t.data_ptr())
+    paths = torch.empty((per, V), dtype=torch.int64, device=dev)
+    for _ in range(args.warmup):
+        ctx.ecmp_counts_device(dist_t.data_ptr(), per, paths.data_ptr())
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    kms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.ecmp_counts_device(dist_t.data_ptr(), per, paths.data_ptr(), timing=True)
+        kms.append(ctx.last_kernel_ms())
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed / args.steps * 1e3
+    kern_ms = float(np.mean(kms))
+    # per destination: dist row read (2V), CSR read (4(V+1) + 4E), counts written (8V)
+    bytes_launch = (hi - lo) * (2 * V + 4 * (V + 1) + 4 * csr.E + 8 * V)
+    achieved = bytes_launch / (kern_ms / 1e3) / 1e9
+    pairs = float(len(dsts)) * V
+    out = {
+        "metric": "ECMP-set sizes of all switch->host-switch pairs (find_route multiple=True), pairs/sec",
+        "value": pairs / (ms / 1e3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "uint64", "data": "synthetic (canonical fabric)",
+        "config": {"workload": "%s shortest-route counts for %d destinations" % (
+            args.fabric, len(dsts)), "fabric": args.fabric, "V": V, "destinations": len(dsts),
+            "max_routes_per_pair": int(paths.max().item()),
+            "parallelism": "destinations sharded over %d GPU(s)" % world},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": ctx.last_kernel(), "kernel_ms": kern_ms,
+                     "bytes_per_launch": bytes_launch},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -255,6 +321,8 @@ def main():
     dev = torch.device("cuda", local)
     if args.mode == "flows":
         return main_flows(args, world, rank, local, dev)
+    if args.mode == "ecmp":
+        return main_ecmp(args, world, rank, local, dev)
 
     fabric = T.by_name(args.fabric)
     csr = fabric.csr()

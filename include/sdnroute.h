@@ -130,6 +130,23 @@ int sdnr_shortest_tables(sdnr_ctx *ctx, const int32_t *dst, int32_t ndst,
  * V <= 16384. */
 int sdnr_apsp(sdnr_ctx *ctx, uint16_t *dist, uint32_t flags);
 
+/* ECMP sets of find_route(src, dst, multiple=True) (_find_routes_bfs,
+ * topology_db.py:86-122: every shortest route, lexicographic dpid order),
+ * counted and unranked instead of enumerated.  dist = sdnr_shortest_tables
+ * rows ([ndst][V], hops toward each destination).
+ * sdnr_ecmp_counts: paths[i*V+x] = number of shortest x -> dst_i routes
+ *   (saturating at UINT64_MAX; 1 at the destination, 0 if unreachable).
+ * sdnr_ecmp_routes: route k = the ranks[k]-th (0-based, lexicographic) shortest
+ *   route from srcs[k] to the destination of row rows[k], as dense vertex ids
+ *   src..dst in route_vertices[k*max_len ...], padded with -1; a row of -1
+ *   if the rank is out of range or the route is longer than max_len. */
+int sdnr_ecmp_counts(sdnr_ctx *ctx, const uint16_t *dist, int32_t ndst,
+                     uint64_t *paths, uint32_t flags);
+int sdnr_ecmp_routes(sdnr_ctx *ctx, const uint16_t *dist, const uint64_t *paths,
+                     int32_t ndst, const int32_t *rows, const int32_t *srcs,
+                     const uint64_t *ranks, int32_t nroutes, int32_t max_len,
+                     int32_t *route_vertices, uint32_t flags);
+
 /* Flow entries of many host pairs from default-route tables (the OFPFlowMods
  * Router._add_flows_for_path installs, reference sdnmpi/router.py:83-104,
  * for the fdb _route_to_fdb builds, sdnmpi/util/topology_db.py:127-138).

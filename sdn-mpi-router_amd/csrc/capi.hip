@@ -527,6 +527,62 @@ int sdnr_route_expand(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port,
     return SDNR_OK;
 }
 
+int sdnr_ecmp_counts(sdnr_ctx *ctx, const uint16_t *dist, int32_t ndst, uint64_t *paths,
+                     uint32_t flags)
+{
+    int rc = begin_call(ctx, 0, nullptr, flags, "sdnr_ecmp_counts");
+    if (rc) return rc;
+    if (ndst < 0 || (ndst > 0 && (!dist || !paths)))
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_ecmp_counts: bad arguments");
+    if (flags & SDNR_DEVICE_PTRS) return sdnr_launch_ecmp_counts(ctx, dist, ndst, paths);
+    const size_t n = (size_t)ndst * ctx->V;
+    if ((rc = sdnr_reserve(&ctx->stage, &ctx->stage_bytes, n * 10 + 512))) return rc;
+    Stage st{static_cast<char *>(ctx->stage)};
+    uint16_t *d_d = static_cast<uint16_t *>(st.take(n * 2));
+    uint64_t *d_p = static_cast<uint64_t *>(st.take(n * 8));
+    SDNR_HIP(hipMemcpyAsync(d_d, dist, n * 2, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = sdnr_launch_ecmp_counts(ctx, d_d, ndst, d_p))) return rc;
+    SDNR_HIP(hipMemcpyAsync(paths, d_p, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    SDNR_HIP(hipStreamSynchronize(ctx->stream));
+    return SDNR_OK;
+}
+
+int sdnr_ecmp_routes(sdnr_ctx *ctx, const uint16_t *dist, const uint64_t *paths, int32_t ndst,
+                     const int32_t *rows, const int32_t *srcs, const uint64_t *ranks,
+                     int32_t nroutes, int32_t max_len, int32_t *route_vertices, uint32_t flags)
+{
+    int rc = begin_call(ctx, 0, nullptr, flags, "sdnr_ecmp_routes");
+    if (rc) return rc;
+    if (ndst < 0 || nroutes < 0 || max_len < 1 ||
+        (nroutes > 0 && (!dist || !paths || !rows || !srcs || !ranks || !route_vertices)))
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_ecmp_routes: bad arguments");
+    if (flags & SDNR_DEVICE_PTRS)
+        return sdnr_launch_ecmp_unrank(ctx, dist, paths, rows, srcs, ranks, nroutes, max_len,
+                                       route_vertices);
+    if ((rc = check_pairs(ctx, ndst, rows, srcs, nroutes, "sdnr_ecmp_routes"))) return rc;
+    const size_t n = (size_t)ndst * ctx->V, r = (size_t)nroutes;
+    const size_t outb = r * (size_t)max_len * 4;
+    if ((rc = sdnr_reserve(&ctx->stage, &ctx->stage_bytes, n * 10 + r * 16 + outb + 2048)))
+        return rc;
+    Stage st{static_cast<char *>(ctx->stage)};
+    uint16_t *d_d = static_cast<uint16_t *>(st.take(n * 2));
+    uint64_t *d_p = static_cast<uint64_t *>(st.take(n * 8));
+    int32_t *d_r = static_cast<int32_t *>(st.take(r * 4));
+    int32_t *d_s = static_cast<int32_t *>(st.take(r * 4));
+    uint64_t *d_k = static_cast<uint64_t *>(st.take(r * 8));
+    int32_t *d_o = static_cast<int32_t *>(st.take(outb));
+    SDNR_HIP(hipMemcpyAsync(d_d, dist, n * 2, hipMemcpyHostToDevice, ctx->stream));
+    SDNR_HIP(hipMemcpyAsync(d_p, paths, n * 8, hipMemcpyHostToDevice, ctx->stream));
+    SDNR_HIP(hipMemcpyAsync(d_r, rows, r * 4, hipMemcpyHostToDevice, ctx->stream));
+    SDNR_HIP(hipMemcpyAsync(d_s, srcs, r * 4, hipMemcpyHostToDevice, ctx->stream));
+    SDNR_HIP(hipMemcpyAsync(d_k, ranks, r * 8, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = sdnr_launch_ecmp_unrank(ctx, d_d, d_p, d_r, d_s, d_k, nroutes, max_len, d_o)))
+        return rc;
+    SDNR_HIP(hipMemcpyAsync(route_vertices, d_o, outb, hipMemcpyDeviceToHost, ctx->stream));
+    SDNR_HIP(hipStreamSynchronize(ctx->stream));
+    return SDNR_OK;
+}
+
 const char *sdnr_last_kernel(const sdnr_ctx *ctx) { return ctx ? ctx->last_kernel : ""; }
 
 int sdnr_last_kernel_ms(sdnr_ctx *ctx, float *ms)

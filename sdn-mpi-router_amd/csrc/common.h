@@ -102,6 +102,11 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
 int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
                          uint16_t *d_dist, int32_t *d_nh, int32_t *d_nh_port);
 int sdnr_launch_apsp(sdnr_ctx *ctx, uint16_t *d_dist);
+int sdnr_launch_ecmp_counts(sdnr_ctx *ctx, const uint16_t *d_dist, int32_t ndst,
+                            uint64_t *d_paths);
+int sdnr_launch_ecmp_unrank(sdnr_ctx *ctx, const uint16_t *d_dist, const uint64_t *d_paths,
+                            const int32_t *d_rows, const int32_t *d_srcs, const uint64_t *d_ranks,
+                            int32_t nroutes, int32_t max_len, int32_t *d_out);
 int sdnr_launch_route_offsets(sdnr_ctx *ctx, const int32_t *d_hops, const int32_t *d_rows,
                               const int32_t *d_dsts, int32_t npairs, int64_t *d_off);
 int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32_t *d_port,

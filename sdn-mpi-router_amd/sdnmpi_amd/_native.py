@@ -34,7 +34,8 @@ EXPORTED_SYMBOLS = (
     "sdnr_abi_version", "sdnr_last_error", "sdnr_device_count", "sdnr_create",
     "sdnr_destroy", "sdnr_set_stream", "sdnr_synchronize", "sdnr_graph_upload",
     "sdnr_graph_info", "sdnr_dfs_tables", "sdnr_dfs_tables_packed", "sdnr_shortest_tables",
-    "sdnr_apsp", "sdnr_route_offsets", "sdnr_route_expand",
+    "sdnr_apsp", "sdnr_route_offsets", "sdnr_route_expand", "sdnr_ecmp_counts",
+    "sdnr_ecmp_routes",
     "sdnr_last_kernel_ms", "sdnr_last_kernel",
 )
 
@@ -75,6 +76,8 @@ def _bind(L):
         "sdnr_shortest_tables": ([vp, vp, i32, vp, vp, vp, u32], c_int),
         "sdnr_apsp": ([vp, vp, u32], c_int),
         "sdnr_route_offsets": ([vp, vp, i32, vp, vp, i32, vp, u32], c_int),
+        "sdnr_ecmp_counts": ([vp, vp, i32, vp, u32], c_int),
+        "sdnr_ecmp_routes": ([vp, vp, vp, i32, vp, vp, vp, i32, i32, vp, u32], c_int),
         "sdnr_route_expand": ([vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp, u32], c_int),
         "sdnr_last_kernel_ms": ([vp, ctypes.POINTER(ctypes.c_float)], c_int),
         "sdnr_last_kernel": ([vp], ctypes.c_char_p),
@@ -242,6 +245,33 @@ class Context(object):
                                            _ptr(dsts), _ptr(last), n, _ptr(off), _ptr(sw),
                                            _ptr(hp), 0))
         return off, sw, hp
+
+    def ecmp_counts(self, dist):
+        """Shortest-route counts uint64 [D, V] from dist rows (saturating)."""
+        dist = np.ascontiguousarray(dist, np.uint16)
+        paths = np.empty(dist.shape, np.uint64)
+        _check(self._lib.sdnr_ecmp_counts(self._h, _ptr(dist), int(dist.shape[0]), _ptr(paths), 0))
+        return paths
+
+    def ecmp_counts_device(self, dist_ptr, ndst, paths_ptr, timing=False):
+        flags = DEVICE_PTRS | (TIMING if timing else 0)
+        _check(self._lib.sdnr_ecmp_counts(self._h, ctypes.c_void_p(dist_ptr), int(ndst),
+                                          ctypes.c_void_p(paths_ptr), flags))
+
+    def ecmp_routes(self, dist, paths, rows, srcs, ranks, max_len):
+        """Vertex sequences int32 [n, max_len] (-1 padded) of the ranks[k]-th
+        lexicographic shortest route from srcs[k] in row rows[k]."""
+        dist = np.ascontiguousarray(dist, np.uint16)
+        paths = np.ascontiguousarray(paths, np.uint64)
+        rows = np.ascontiguousarray(rows, np.int32)
+        srcs = np.ascontiguousarray(srcs, np.int32)
+        ranks = np.ascontiguousarray(ranks, np.uint64)
+        n = int(rows.shape[0])
+        out = np.empty((n, int(max_len)), np.int32)
+        _check(self._lib.sdnr_ecmp_routes(self._h, _ptr(dist), _ptr(paths), int(dist.shape[0]),
+                                          _ptr(rows), _ptr(srcs), _ptr(ranks), n, int(max_len),
+                                          _ptr(out), 0))
+        return out
 
     def route_offsets_device(self, hops_ptr, rows_ptr, dsts_ptr, npairs, off_ptr):
         _check(self._lib.sdnr_route_offsets(self._h, ctypes.c_void_p(hops_ptr), 0,

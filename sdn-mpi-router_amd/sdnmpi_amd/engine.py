@@ -39,6 +39,29 @@ class RouteEngine(object):
         self.load(export)
         return self.ctx.shortest_tables(dsts, with_nexthop=True)
 
+    def ecmp(self, export, dist, rows, srcs):
+        """Every shortest route of each (rows[i], srcs[i]) pair, lexicographic
+        order (ecmp.hip): list of int32 [n_i, len_i] vertex arrays."""
+        self.load(export)
+        paths = self.ctx.ecmp_counts(dist)
+        rows = np.asarray(rows, np.int64)
+        srcs = np.asarray(srcs, np.int64)
+        cnt = paths[rows, srcs].astype(np.int64)
+        if (paths[rows, srcs] > np.uint64(1 << 40)).any():
+            raise MemoryError("ECMP set too large to enumerate")
+        lens = dist[rows, srcs].astype(np.int64) + 1
+        rr = np.repeat(rows, cnt)
+        ss = np.repeat(srcs, cnt)
+        starts = np.cumsum(cnt) - cnt
+        ranks = np.arange(int(cnt.sum()), dtype=np.int64) - np.repeat(starts, cnt)
+        max_len = int(lens[cnt > 0].max()) if (cnt > 0).any() else 1
+        verts = self.ctx.ecmp_routes(dist, paths, rr, ss, ranks.astype(np.uint64), max_len)
+        out, k = [], 0
+        for i in range(rows.shape[0]):
+            out.append(verts[k:k + cnt[i], :lens[i]] if cnt[i] else verts[0:0, :0])
+            k += int(cnt[i])
+        return out
+
     def expand(self, export, tables, rows, dsts, last_port):
         """Flow entries of many pairs (routes.hip): (offsets, switch ids, ports)."""
         self.load(export)

@@ -245,6 +245,38 @@ class TopologyDB(object):
                     "dpids": ex.csr.dpids}
         raise ValueError("mode must be 'dfs' or 'shortest'")
 
+    def _find_routes_multiple(self, pairs):
+        """find_route(a, b, multiple=True) for many pairs: per-destination
+        distances from the GPU tables, the ECMP sets counted and unranked on the
+        GPU (ecmp.hip), each route turned into its fdb as _route_to_fdb does."""
+        ex = self.graph()
+        n = len(pairs)
+        ends = [None] * n
+        want = []
+        for i, (a, b) in enumerate(pairs):
+            ea, eb = self._endpoint(a), self._endpoint(b)
+            if ea is None or eb is None:
+                continue
+            s, d = ex.index[ea[0]], ex.index[eb[0]]
+            ends[i] = (s, d, self._last_hop(eb[0], eb[1], b))
+            want.append(d)
+        out = [[] for _ in range(n)]
+        if not want:
+            return out
+        batch = self._host_vertices(ex) if self._batch else ()
+        tabs = self._cache.sp_rows(self.engine, sorted(set(want)), batch)
+        dist = tabs[0]
+        idx = [i for i in range(n) if ends[i] is not None]
+        rows = [self._cache.sp_row[ends[i][1]] for i in idx]
+        srcs = [ends[i][0] for i in idx]
+        # only the destination rows these pairs use go to the GPU
+        urows, inv = np.unique(np.asarray(rows, np.int64), return_inverse=True)
+        sets = self.engine.ecmp(ex, dist[urows], inv, srcs)
+        for i, seqs in zip(idx, sets):
+            last = ends[i][2]
+            out[i] = [self._seq_fdb(ex, [int(v) for v in q], last) for q in seqs]
+        return out
+
     def route_entries(self, pairs):
         """Flow entries of many (src_mac, dst_mac) pairs in one GPU pass --
         what ``Router._add_flows_for_path`` installs for each pair (reference
@@ -287,6 +319,8 @@ class TopologyDB(object):
         once for all of them, and the default-route fdbs of large batches are
         expanded on the GPU (``route_entries``)."""
         pairs = list(pairs)
+        if multiple and len(pairs) >= 16:
+            return self._find_routes_multiple(pairs)
         if not multiple and len(pairs) >= 64:
             off, dp, pt = self.route_entries(pairs)
             dp, pt = dp.tolist(), pt.tolist()

@@ -156,6 +156,17 @@ class _FakeEngine(object):
         self.calls.append(("sp", export.key, tuple(int(x) for x in dsts)))
         return self.O.dest_tables(export.csr, dsts)
 
+    def ecmp(self, export, dist, rows, srcs):
+        # host walk of the shortest-path DAG (test double only)
+        from sdnmpi_amd.engine import shortest_paths_lex
+        c = export.csr
+        out = []
+        for r, s in zip(rows, srcs):
+            d = int(np.nonzero(dist[r] == 0)[0][0])
+            q = shortest_paths_lex(c.row_ptr, c.col, dist[r], int(s), d)
+            out.append(np.asarray(q, np.int32).reshape(len(q), -1))
+        return out
+
     def expand(self, export, tables, rows, dsts, last_port):
         # numpy restatement of routes.hip (test double only)
         from sdnmpi_amd.engine import expand_tree_paths
@@ -312,3 +323,43 @@ def test_route_entries_k48_golden_pairs():
     macs = fabric.host_macs()
     got = db.find_routes([(macs[int(a)], macs[int(b)]) for a, b in zip(g.pair_src, g.pair_dst)])
     assert got == [g.fdb(i) for i in range(len(g))]
+
+
+def test_find_routes_multiple_batched_fake_engine():
+    from oracle import oracle as O
+    from sdnmpi_amd import topologies as T
+    fabric = T.fat_tree(4)
+    db = fabric.populate(TopologyDB())
+    db._engine = _FakeEngine()
+    macs = fabric.host_macs() + ["00:00:00:00:00:05", "02:00:00:00:00:77"]
+    pairs = [(a, b) for a in macs[::3] for b in macs]
+    assert db.find_routes(pairs, True) == [O.find_routes_all_shortest(db, a, b) for a, b in pairs]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", G.MULTI)
+def test_ecmp_sets_match_reference(name):
+    """GPU-counted and -unranked ECMP sets equal the reference's
+    find_route(..., multiple=True) lists (golden fixtures)."""
+    g = G.Golden(name)
+    fabric = g.fabric()
+    db = fabric.populate(TopologyDB())
+    macs = fabric.host_macs()
+    pairs = [(macs[int(a)], macs[int(b)]) for a, b in zip(g.pair_src, g.pair_dst)]
+    assert db.find_routes(pairs * (1 if len(pairs) >= 16 else 16), True)[:len(pairs)] == \
+        [g.multi(i) for i in range(len(g))]
+
+
+@pytest.mark.gpu
+def test_ecmp_sets_k48_sampled():
+    """k=48: 576 shortest routes per inter-pod pair, vs the host walk of the
+    oracle's shortest-path DAG (the reference itself cannot enumerate them)."""
+    from oracle import oracle as O
+    g = G.Golden("fat_tree_k48_sample")
+    fabric = g.fabric()
+    db = fabric.populate(TopologyDB())
+    macs = fabric.host_macs()
+    pairs = [(macs[int(a)], macs[int(b)]) for a, b in zip(g.pair_src[:40], g.pair_dst[:40])]
+    got = db.find_routes(pairs, True)
+    assert got == [O.find_routes_all_shortest(db, a, b) for a, b in pairs]
+    assert max(len(r) for r in got) == 576
