@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--fabric", default="fat_tree:48")
-    ap.add_argument("--mode", choices=["dfs", "shortest", "flows", "ecmp"], default="dfs")
+    ap.add_argument("--mode", choices=["dfs", "shortest", "flows", "ecmp", "apsp"], default="dfs")
     ap.add_argument("--ranks", type=int, default=1024,
                     help="flows mode: MPI ranks placed on random hosts; every ordered "
                          "rank pair's flow entries are emitted per step")
@@ -302,6 +302,55 @@ def main_ecmp(args, world, rank, local, dev):
         dist.destroy_process_group()
 
 
+def main_apsp(args, world, rank, local, dev):
+    """All-pairs hop distances by the blocked min-plus closure (apsp.hip) --
+    the north star's small-dense-fabric kernel; every switch pair's hop count
+    of find_route(..., multiple=True).  One step = the full V x V matrix;
+    value = switch pairs per second; bound: the VALU min/add rate (min-plus is
+    not a multiply-accumulate, so MFMA does not apply), reported against the
+    packed-u16 VALU peak."""
+    fabric = T.by_name(args.fabric)
+    csr = fabric.csr()
+    V = csr.V
+    ctx = _native.Context(local)
+    ctx.upload(csr)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream.cuda_stream)
+    d = torch.empty((V, V), dtype=torch.int16, device=dev)
+    for _ in range(args.warmup):
+        ctx.apsp_device(d.data_ptr())
+    torch.cuda.synchronize(dev)
+    kms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.apsp_device(d.data_ptr(), timing=True)
+        kms.append(ctx.last_kernel_ms())
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) / args.steps * 1e3
+    kern_ms = float(np.mean(kms))
+    nb = (V + 63) // 64
+    Vp = nb * 64
+    ops = 2.0 * Vp ** 3                     # one add + one min per (i, j, k)
+    achieved = ops / (kern_ms / 1e3) / 1e12
+    # VALU peak: 256 CUs x 4 SIMDs x 32 lanes x 2 (packed u16) ops/clk x 2.4 GHz
+    peak = 256 * 4 * 32 * 2 * 2.4e9 / 1e12
+    out = {
+        "metric": "all-pairs hop distances (blocked min-plus APSP), switch pairs/sec",
+        "value": float(V) * V / (ms / 1e3), "unit": "pairs/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u16",
+        "data": "synthetic (canonical fabric)",
+        "config": {"workload": "%s APSP (V=%d)" % (args.fabric, V), "fabric": args.fabric, "V": V},
+        "roofline": {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "Tops/s",
+                     "frac": achieved / peak, "traffic": None, "kernel": ctx.last_kernel(),
+                     "kernel_ms": kern_ms, "ops_per_launch": ops},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -323,6 +372,8 @@ def main():
         return main_flows(args, world, rank, local, dev)
     if args.mode == "ecmp":
         return main_ecmp(args, world, rank, local, dev)
+    if args.mode == "apsp":
+        return main_apsp(args, world, rank, local, dev)
 
     fabric = T.by_name(args.fabric)
     csr = fabric.csr()

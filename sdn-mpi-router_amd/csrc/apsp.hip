@@ -10,6 +10,9 @@
 // itself, (2) pivot row and column tiles close against it, (3) every other
 // tile takes one min-plus product.  Distances saturate at 0xFFFF (= no
 // path), the same convention as the msbfs dist tables it cross-checks.
+#include <stdlib.h>
+#include <string.h>
+
 #include "common.h"
 
 namespace {
@@ -134,21 +137,192 @@ __global__ __launch_bounds__(256) void apsp_phase3_kernel(int Vp, int kb, uint16
                 (uint16_t)(acc[r][c] > INF ? INF : acc[r][c]);
 }
 
+// ---------------------------------------------------------------------------
+// Min-plus squaring: D <- min(D, D (x) D) in place, repeated until nothing
+// changes.  Unlike the blocked Floyd-Warshall above (three dependent phases
+// and 64 serial pivots per block step) every squaring is one fully parallel
+// GEMM-shaped launch, and hop distances of a fabric with diameter d need
+// ceil(log2 d) + 1 of them (k=48: 3).  In place is exact: every entry is
+// always the length of some path (reading an already-improved value only
+// speeds convergence), and a pass that improves nothing is the closure.
+// The arithmetic is packed u16 on the VALU -- v_pk_add_u16 with clamp (0xFFFF
+// saturates as "no path") and v_pk_min_u16 -- 2 (i, j) pairs per lane per
+// instruction; each thread owns an 8 x 8 output block of a 128 x 128 tile,
+// K staged through LDS in 32-wide slices, k-major so the 8 A values and the
+// 8 B values of a step are one ds_read_b128 each.
+// ---------------------------------------------------------------------------
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int MT = 128;          // output tile edge
+constexpr int KS = 32;           // K slice
+constexpr int LDA = MT + 8;      // padded LDS row (u16)
+
+__device__ __forceinline__ u16x2 as_pk(uint32_t x)
+{
+    return __builtin_bit_cast(u16x2, x);
+}
+
+__device__ __forceinline__ uint32_t as_u32(u16x2 x)
+{
+    return __builtin_bit_cast(uint32_t, x);
+}
+
+__global__ __launch_bounds__(256) void minplus_square_kernel(int Vp, uint16_t *__restrict__ D,
+                                                             int *__restrict__ changed)
+{
+    __shared__ __attribute__((aligned(16))) uint16_t As[KS][LDA];   // As[k][i] = D[i0+i][k0+k]
+    __shared__ __attribute__((aligned(16))) uint16_t Bs[KS][LDA];   // Bs[k][j] = D[k0+k][j0+j]
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int i0 = blockIdx.y * MT, j0 = blockIdx.x * MT;
+    u16x2 acc[8][4];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(D + (size_t)(i0 + ty * 8 + r) * Vp + j0 + tx * 8);
+        acc[r][0] = as_pk(v.x);
+        acc[r][1] = as_pk(v.y);
+        acc[r][2] = as_pk(v.z);
+        acc[r][3] = as_pk(v.w);
+    }
+
+    // slices are staged register -> LDS: the next slice's global loads are in
+    // flight while the current one is consumed
+    uint4 ra[2], rb[2];
+    auto load_slice = [&](int k0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int L = threadIdx.x + 256 * h;
+            ra[h] = *reinterpret_cast<const uint4 *>(D + (size_t)(i0 + (L >> 2)) * Vp + k0 +
+                                                      (L & 3) * 8);
+            rb[h] = *reinterpret_cast<const uint4 *>(D + (size_t)(k0 + (L >> 4)) * Vp + j0 +
+                                                      (L & 15) * 8);
+        }
+    };
+    auto store_slice = [&]() {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int L = threadIdx.x + 256 * h;
+            const int i = L >> 2, kq = (L & 3) * 8;          // A: transpose into As[k][i]
+            const uint32_t w[4] = {ra[h].x, ra[h].y, ra[h].z, ra[h].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                As[kq + 2 * e][i] = (uint16_t)(w[e] & 0xFFFFu);
+                As[kq + 2 * e + 1][i] = (uint16_t)(w[e] >> 16);
+            }
+            *reinterpret_cast<uint4 *>(&Bs[L >> 4][(L & 15) * 8]) = rb[h];   // B: k-major already
+        }
+    };
+    load_slice(0);
+    for (int k0 = 0; k0 < Vp; k0 += KS) {
+        store_slice();
+        __syncthreads();
+        if (k0 + KS < Vp) load_slice(k0 + KS);
+#pragma unroll 4
+        for (int k = 0; k < KS; ++k) {
+            const uint4 av = *reinterpret_cast<const uint4 *>(&As[k][ty * 8]);
+            const uint4 bv = *reinterpret_cast<const uint4 *>(&Bs[k][tx * 8]);
+            const u16x2 b[4] = {as_pk(bv.x), as_pk(bv.y), as_pk(bv.z), as_pk(bv.w)};
+            const uint32_t aw[4] = {av.x, av.y, av.z, av.w};
+            // splat a row's value into both halves with one v_perm_b32, then
+            // all 32 saturating adds before the 32 mins
+            u16x2 t[8][4];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const u16x2 as = as_pk(__builtin_amdgcn_perm(aw[r >> 1], aw[r >> 1],
+                                                             (r & 1) ? 0x03020302u : 0x01000100u));
+#pragma unroll
+                for (int c = 0; c < 4; ++c) t[r][c] = __builtin_elementwise_add_sat(as, b[c]);
+            }
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) acc[r][c] = __builtin_elementwise_min(acc[r][c], t[r][c]);
+        }
+        __syncthreads();
+    }
+    // only this block writes its tile, so the old values can be re-read here
+    // instead of being held in registers through the K loop
+    bool any = false;
+    uint32_t mx = 0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        uint16_t *p = D + (size_t)(i0 + ty * 8 + r) * Vp + j0 + tx * 8;
+        const uint4 o = *reinterpret_cast<const uint4 *>(p);
+        uint4 v;
+        v.x = as_u32(acc[r][0]);
+        v.y = as_u32(acc[r][1]);
+        v.z = as_u32(acc[r][2]);
+        v.w = as_u32(acc[r][3]);
+        any |= (v.x != o.x) | (v.y != o.y) | (v.z != o.z) | (v.w != o.w);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t w = as_u32(acc[r][c]);
+            const uint32_t lo = w & 0xFFFFu, hi = w >> 16;
+            mx = max(mx, lo == 0xFFFFu ? 0u : lo);
+            mx = max(mx, hi == 0xFFFFu ? 0u : hi);
+        }
+        *reinterpret_cast<uint4 *>(p) = v;
+    }
+    if (__ballot(any) && lane_id() == 0) atomicOr(changed, 1);
+    // largest finite distance (wave max, one atomic per wave)
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    if (lane_id() == 0) atomicMax(reinterpret_cast<unsigned *>(changed) + 1, mx);
+}
+
 }  // namespace
+
+static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp)
+{
+    int rc = sdnr_reserve(&ctx->scratch2, &ctx->scratch2_bytes, 256);
+    if (rc) return rc;
+    int *changed = static_cast<int *>(ctx->scratch2);
+    hipLaunchKernelGGL(apsp_init_kernel, dim3(1024), dim3(256), 0, ctx->stream, V, Vp,
+                       ctx->row_ptr, ctx->col, D);
+    hipLaunchKernelGGL(apsp_edges_kernel, dim3((V + 255) / 256), dim3(256), 0, ctx->stream, V, Vp,
+                       ctx->row_ptr, ctx->col, D);
+    // stop when a pass changes nothing, or when after s squarings (exact for
+    // every distance <= 2^s) the largest finite distance M is < 2^s: no pair
+    // is at distance M + 1 <= 2^s, so none is farther
+    const int nt = Vp / MT;
+    for (int it = 1; it <= 40; ++it) {         // 2^40 >> any hop distance
+        SDNR_HIP(hipMemsetAsync(changed, 0, 2 * sizeof(int), ctx->stream));
+        hipLaunchKernelGGL(minplus_square_kernel, dim3(nt, nt), dim3(256), 0, ctx->stream, Vp, D,
+                           changed);
+        SDNR_HIP(hipGetLastError());
+        int h[2] = {0, 0};
+        SDNR_HIP(hipMemcpyAsync(h, changed, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        SDNR_HIP(hipStreamSynchronize(ctx->stream));
+        if (!h[0] || (it < 31 && (long long)h[1] < (1ll << it))) break;
+    }
+    return SDNR_OK;
+}
 
 int sdnr_launch_apsp(sdnr_ctx *ctx, uint16_t *d_dist)
 {
     const int V = ctx->V;
     if (V == 0) return SDNR_OK;
     if (V > 16384) return sdnr_fail(SDNR_ERR_INVAL, "apsp: V=%d > 16384", V);
-    const int nb = (V + T - 1) / T;
-    const int Vp = nb * T;
+    // SDNROUTE_APSP=fw selects the blocked Floyd-Warshall (A/B, tests)
+    const char *f = getenv("SDNROUTE_APSP");
+    const bool fw = f && !strcmp(f, "fw");
+    const int nb = (V + (fw ? T : MT) - 1) / (fw ? T : MT);
+    const int Vp = nb * (fw ? T : MT);
     const size_t bytes = (size_t)Vp * Vp * sizeof(uint16_t);
     uint16_t *D = d_dist;
     if (Vp != V) {
         int rc = sdnr_reserve(&ctx->scratch, &ctx->scratch_bytes, bytes);
         if (rc) return rc;
         D = static_cast<uint16_t *>(ctx->scratch);
+    }
+    if (!fw) {
+        ctx->last_kernel = "minplus_square_kernel";
+        if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
+        int rc = launch_apsp_squaring(ctx, D, V, Vp);
+        if (rc) return rc;
+        if (D != d_dist)
+            SDNR_HIP(hipMemcpy2DAsync(d_dist, (size_t)V * 2, D, (size_t)Vp * 2, (size_t)V * 2, V,
+                                      hipMemcpyDeviceToDevice, ctx->stream));
+        if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+        return SDNR_OK;
     }
     ctx->last_kernel = "apsp_phase{1,2,3}_kernel";
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));

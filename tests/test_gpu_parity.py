@@ -244,9 +244,12 @@ def test_shortest_global_path_torus(ctx):
     np.testing.assert_array_equal(nhp, nhpo)
 
 
+@pytest.mark.parametrize("algo", ["squaring", "fw"])
 @pytest.mark.parametrize("name", ["mock", "fat_tree_k8", "dragonfly_a4_h2_p2",
-                                  "random_V60_dense", "torus_5x3x2"])
-def test_apsp_small(ctx, name):
+                                  "random_V60_dense", "torus_5x3x2", "random_V40", "random_V9"])
+def test_apsp_small(ctx, monkeypatch, name, algo):
+    if algo == "fw":
+        monkeypatch.setenv("SDNROUTE_APSP", "fw")
     csr = G.Golden(name).fabric().csr()
     ctx.upload(csr)
     np.testing.assert_array_equal(ctx.apsp(), O.apsp(csr))
@@ -278,6 +281,22 @@ def test_shortest_unknown_destination_rows_device(ctx):
     d = dist.cpu().numpy().view(np.uint16)
     assert (d[0] == 0xFFFF).all() and (d[2] == 0xFFFF).all() and d[1, 3] == 0
     assert (nh.cpu().numpy()[[0, 2]] == -1).all()
+
+
+def test_apsp_fullsize_k48_matches_bfs(ctx):
+    csr = T.fat_tree(48).csr()
+    ctx.upload(csr)
+    D = ctx.apsp()
+    assert ctx.last_kernel() == "minplus_square_kernel"
+    dist, _, _ = ctx.shortest_tables(np.arange(csr.V, dtype=np.int32), with_nexthop=False)
+    np.testing.assert_array_equal(D.T, dist)
+
+
+def test_apsp_long_paths_torus(ctx):
+    """A high-diameter graph (ring-like torus 40x3x1): many squarings."""
+    csr = T.torus3d(40, 3, 1).csr()
+    ctx.upload(csr)
+    np.testing.assert_array_equal(ctx.apsp(), O.apsp(csr))
 
 
 def test_apsp_matches_msbfs_dragonfly(ctx):
