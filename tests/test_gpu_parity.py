@@ -377,3 +377,37 @@ def test_edge_graphs(ctx):
     port = np.arange(len(col))
     star = CSR(np.arange(1, V + 1), rp, col, port)
     _check_dfs(ctx, star, np.arange(V, dtype=np.int32))
+
+
+def test_new_paths_on_edge_graphs(ctx):
+    """Isolated vertices, a one-way link and an unreachable destination
+    through the route expansion, ECMP and APSP entry points."""
+    from sdnmpi_amd.topologies import CSR
+    # 0 -> 1 (port 5), 2 isolated
+    c = CSR(np.array([3, 7, 9]), np.array([0, 1, 1, 1]), np.array([1]), np.array([5]))
+    ctx.upload(c)
+    p, t, h = ctx.dfs_tables(np.arange(3, dtype=np.int32))
+    off, sw, hp = ctx.expand_routes(p, t, h, np.array([0, 0, 1, 2]), np.array([1, 2, 0, 2]),
+                                    np.array([11, 12, 13, 14]))
+    assert off.tolist() == [0, 2, 2, 2, 3]
+    assert sw.tolist() == [0, 1, 2] and hp.tolist() == [5, 11, 14]
+    dist, nh, nhp = ctx.shortest_tables(np.arange(3, dtype=np.int32))
+    paths = ctx.ecmp_counts(dist)
+    assert paths[1].tolist() == [1, 1, 0] and paths[2].tolist() == [0, 0, 1]
+    r = ctx.ecmp_routes(dist, paths, np.array([1, 1, 0]), np.array([0, 2, 1]),
+                        np.array([0, 0, 0], np.uint64), 3)
+    assert r.tolist() == [[0, 1, -1], [-1, -1, -1], [-1, -1, -1]]
+    np.testing.assert_array_equal(ctx.apsp(), O.apsp(c))
+
+
+def test_ecmp_counts_match_dag_walk_dragonfly(ctx):
+    from sdnmpi_amd.engine import shortest_paths_lex
+    csr = T.dragonfly(4, 2, 2).csr()
+    ctx.upload(csr)
+    dsts = np.arange(csr.V, dtype=np.int32)
+    dist, _, _ = ctx.shortest_tables(dsts)
+    paths = ctx.ecmp_counts(dist)
+    for d in range(0, csr.V, 3):
+        for x in range(csr.V):
+            seqs = shortest_paths_lex(csr.row_ptr, csr.col, dist[d], x, d)
+            assert paths[d, x] == len(seqs)
