@@ -293,12 +293,29 @@ int sdnr_graph_upload(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_pt
             return sdnr_hip_fail(he, "graph_upload(adj16)");
         }
     }
+    // symmetric (every link has its reverse): in-rows equal out-rows, so a
+    // BFS toward a destination may expand out-rows
+    bool symmetric = true;
+    for (int32_t u = 0; u < V && symmetric; ++u)
+        for (int32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) {
+            const int32_t v = col[e];
+            int32_t lo = row_ptr[v], hi = row_ptr[v + 1];
+            while (lo < hi) {
+                const int32_t mid = (lo + hi) >> 1;
+                if (col[mid] < u) lo = mid + 1; else hi = mid;
+            }
+            if (lo == row_ptr[v + 1] || col[lo] != u) {
+                symmetric = false;
+                break;
+            }
+        }
     SDNR_HIP(hipStreamSynchronize(ctx->stream));
     ctx->V = V;
     ctx->E = E;
     ctx->W = W;
     ctx->max_deg = maxdeg;
     ctx->port16 = port16;
+    ctx->symmetric = symmetric;
     return SDNR_OK;
 }
 

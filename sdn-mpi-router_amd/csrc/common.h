@@ -65,6 +65,7 @@ struct sdnr_ctx {
     void *scratch2 = nullptr;           // int32 tables behind a packed-table call
     size_t scratch2_bytes = 0;
     bool port16 = false;                // every port fits the packed layout (< 0xFFFF)
+    bool symmetric = false;             // every link (u, v) has its reverse (v, u)
 
     // timing of the main kernel(s) of the last SDNR_TIMING call
     hipEvent_t ev0 = nullptr, ev1 = nullptr;

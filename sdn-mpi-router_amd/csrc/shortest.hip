@@ -92,19 +92,20 @@ __global__ __launch_bounds__(256) void msbfs_level_kernel(
     uint64_t *__restrict__ next, uint64_t *__restrict__ vis, uint16_t *__restrict__ dist,
     int *__restrict__ changed)
 {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int x0 = blockIdx.x * blockDim.x + threadIdx.x;
     const int batch = blockIdx.y;
-    if (x >= V) return;
+    // every lane stays to the end (the distance stores below are a wave-wide
+    // loop); lanes past V work on vertex V-1 and store nothing
+    const bool live = x0 < V;
+    const int x = live ? x0 : V - 1;
     const size_t off = (size_t)batch * V;
     const int nb = min(64, ndst - batch * 64);
     const uint64_t all = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
     const uint64_t vx = vis[off + x];
-    if ((vx & all) == all) {                  // nothing left to reach at x
-        next[off + x] = 0;
-        return;
-    }
     uint64_t acc = 0;
-    if (W > 0) {
+    if (!live || (vx & all) == all) {         // nothing left to reach at x
+        acc = 0;
+    } else if (W > 0) {
         const int32_t *r = ell_col + (size_t)x * W;
         for (int j = 0; j < W; ++j) {
             const int n = r[j];
@@ -114,12 +115,27 @@ __global__ __launch_bounds__(256) void msbfs_level_kernel(
         const int re = row_ptr[x + 1];
         for (int e = row_ptr[x]; e < re; ++e) acc |= front[off + col[e]];
     }
-    const uint64_t nw = acc & ~vx;
-    next[off + x] = nw;
+    const uint64_t nw = live ? acc & ~vx : 0ull;
+    if (live) next[off + x] = nw;
     if (nw) {
         vis[off + x] = vx | nw;
-        write_levels(nw, batch * 64, ndst, V, x, (uint16_t)lvl, dist);
         *changed = 1;
+    }
+    // distances: iterate the destinations any lane of the wave reached, so
+    // each store instruction writes one destination row at consecutive x
+    // (coalesced) instead of every lane walking its own bits
+    uint32_t lo = (uint32_t)nw, hi = (uint32_t)(nw >> 32);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        lo |= (uint32_t)__shfl_xor((int)lo, o);
+        hi |= (uint32_t)__shfl_xor((int)hi, o);
+    }
+    uint64_t any = ((uint64_t)hi << 32) | lo;
+    const int b0 = batch * 64;
+    while (any) {
+        const int b = __ffsll((unsigned long long)any) - 1;
+        any &= any - 1;
+        if (((nw >> b) & 1ull) && b0 + b < ndst) dist[(size_t)(b0 + b) * V + x] = (uint16_t)lvl;
     }
 }
 

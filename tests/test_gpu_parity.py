@@ -231,6 +231,20 @@ def test_shortest_fullsize_fat_tree(ctx, monkeypatch, strategy):
     np.testing.assert_array_equal(nhp, nhpo)
 
 
+def test_shortest_fullsize_torus_sample(ctx):
+    """torus 32^3 (the BASELINE multi-source BFS config), spread destinations."""
+    fabric = T.torus3d(32, 32, 32)
+    csr = fabric.csr()
+    dsts = np.linspace(0, csr.V - 1, 96).astype(np.int32)
+    ctx.upload(csr)
+    dist, nh, nhp = ctx.shortest_tables(dsts)
+    assert ctx.last_kernel().startswith("msbfs_level_kernel")
+    do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
+    np.testing.assert_array_equal(dist, do)
+    np.testing.assert_array_equal(nh, nho)
+    np.testing.assert_array_equal(nhp, nhpo)
+
+
 def test_shortest_global_path_torus(ctx):
     """V > 6400 -> masks in HBM, one launch per level."""
     fabric = T.torus3d(24, 24, 16)
