@@ -60,6 +60,7 @@ class TopologyDB(object):
         self._export = None
         self._cache = None
         self._hv = (None, None)          # (version key, host vertices)
+        self._lp = (None, None)          # (links version, link endpoint ports)
         # Switch DPID -> Switch; src DPID -> dst DPID -> Link; MAC -> Host
         self.switches = {}
         self.links = {}
@@ -220,6 +221,33 @@ class TopologyDB(object):
             out.append((int(c.dpids[a]), int(c.port[e])))
         out.append(last)
         return out
+
+    # -- flood helper --------------------------------
+    def _link_ports(self):
+        """{(dpid, port_no)} of every link endpoint, rebuilt when ``links``
+        changes (one pass over the links instead of one per query)."""
+        key = self._versions.links
+        if self._lp[0] != key:
+            ends = set()
+            for nb in self.links.values():
+                for lk in nb.values():
+                    ends.add((lk.src.dpid, lk.src.port_no))
+                    ends.add((lk.dst.dpid, lk.dst.port_no))
+            self._lp = (key, ends)
+        return self._lp[1]
+
+    def is_edge_port(self, port):
+        """``TopologyManager._is_edge_port`` (reference sdnmpi/topology.py:
+        150-155): the port is neither end of any link.  O(1) per query."""
+        return (port.dpid, port.port_no) not in self._link_ports()
+
+    def edge_ports(self, switch, in_port=None):
+        """The ports ``_do_broadcast`` floods on ``switch`` (topology.py:
+        157-168): edge ports that are not reserved, minus ``in_port``."""
+        ends = self._link_ports()
+        return [p for p in switch.ports
+                if (p.dpid, p.port_no) not in ends and not p.is_reserved()
+                and (in_port is None or p.port_no != in_port)]
 
     # -- batched (all-pairs) interface ---------------------------------
     def route_tables(self, mode="dfs"):

@@ -363,3 +363,46 @@ def test_ecmp_sets_k48_sampled():
     got = db.find_routes(pairs, True)
     assert got == [O.find_routes_all_shortest(db, a, b) for a, b in pairs]
     assert max(len(r) for r in got) == 576
+
+
+def test_edge_port_helpers_match_reference_loop():
+    """is_edge_port / edge_ports vs the reference's O(links) loop
+    (sdnmpi/topology.py:150-168), before and after link changes."""
+    from sdnmpi_amd import topologies as T
+    from sdnmpi_amd.objects import Switch
+
+    def ref_is_edge(db, port):            # topology.py:150-155, restated
+        for nb in db.links.values():
+            for lk in nb.values():
+                if port == lk.src or port == lk.dst:
+                    return False
+        return True
+
+    fabric = T.fat_tree(4)
+    db = fabric.populate(TopologyDB())
+    ports = {}
+    for nb in db.links.values():
+        for lk in nb.values():
+            ports.setdefault(lk.src.dpid, set()).add(lk.src.port_no)
+    for h in db.hosts.values():
+        ports.setdefault(h.port.dpid, set()).add(h.port.port_no)
+    sws = []
+    for d in sorted(ports):
+        sw = Switch(d)
+        sw.ports = [Port(d, n) for n in sorted(ports[d])] + [Port(d, 0xfffe)]
+        sws.append(sw)
+
+    def check():
+        for sw in sws:
+            for p in sw.ports:
+                assert db.is_edge_port(p) == ref_is_edge(db, p)
+            want = [p for p in sw.ports if ref_is_edge(db, p) and not p.is_reserved()
+                    and p.port_no != 3]
+            assert db.edge_ports(sw, in_port=3) == want
+
+    check()
+    lk = next(iter(db.links[sws[-1].dp.id].values()))
+    db.delete_link(lk)
+    check()
+    del db.links[lk.dst.dpid]
+    check()
