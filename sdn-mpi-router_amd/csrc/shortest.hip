@@ -234,7 +234,7 @@ constexpr uint32_t kSentLevel = 0xFFFEu;        // level of the padding vertex V
 __host__ __device__ inline int bfs_dest_qwords(int V) { return ((V + 1) / 2 + 3) & ~3; }
 __host__ __device__ inline int bfs_dest_words(int V)
 {
-    return ((V + 1 + 255) & ~255) + 2 * bfs_dest_qwords(V) + (((V + 3) / 4 + 3) & ~3) + 4;
+    return ((V + 1 + 255) & ~255) + 2 * bfs_dest_qwords(V) + (((V + 3) / 4 + 3) & ~3) + 8;
 }
 
 template <int NW, int G, bool SYM>
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(NW * 64) void bfs_dest_kernel(
     uint16_t *q = reinterpret_cast<uint16_t *>(lvl + DWp);            // BFS order
     uint16_t *nhv = reinterpret_cast<uint16_t *>(lvl + DWp + QWp);    // next hop
     uint8_t *nhs = reinterpret_cast<uint8_t *>(lvl + DWp + 2 * QWp);  // its row slot
-    int *ctl = reinterpret_cast<int *>(lds + bfs_dest_words(V) - 4);  // [0] queue tail
+    int *ctl = reinterpret_cast<int *>(lds + bfs_dest_words(V) - 8);  // per-wave counts
     const uint16_t *inrow = SYM ? adj : radj;
     const int lane = lane_id();
     const int w = uniform((int)(threadIdx.x >> 6));
@@ -276,15 +276,16 @@ __global__ __launch_bounds__(NW * 64) void bfs_dest_kernel(
         }
         for (int i = threadIdx.x; i <= V; i += blockDim.x)
             lvl[lds_swz(i)] = i == d ? 0u : (i == V ? kSentLevel : kUnseen);
-        if (threadIdx.x == 0) {
-            q[0] = (uint16_t)d;
-            ctl[0] = 1;
-        }
+        if (threadIdx.x == 0) q[0] = (uint16_t)d;
         __syncthreads();
 
         int lo = 0, hi = 1;
+        const int slice = ((V + NW * 64 - 1) / (NW * 64)) * 64;   // scan slice per wave
         for (int L = 0; lo < hi; ++L) {
-            // ---- expand level L = q[lo, hi): G rows per wave in flight
+            // ---- expand level L = q[lo, hi): G rows per wave in flight.
+            // Unseen in-neighbours take level L+1 with a plain store (every
+            // writer stores the same value); no claim round trip, no queue
+            // atomic -- the next frontier is collected by the scan below.
             for (int base = lo + w * G; base < hi; base += NW * G) {
                 const int n = min(G, hi - base);
                 const int mine = lane < n ? (int)q[base + lane] : V;   // past n: sentinel row
@@ -295,56 +296,54 @@ __global__ __launch_bounds__(NW * 64) void bfs_dest_kernel(
                 uint32_t lv[G];
 #pragma unroll
                 for (int g = 0; g < G; ++g) lv[g] = lvl[lds_swz(r[g])];
-                uint32_t old[G];
 #pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    old[g] = kSentLevel;
-                    if (lv[g] == kUnseen)
-                        old[g] = atomicCAS(&lvl[lds_swz(r[g])], kUnseen, (uint32_t)(L + 1));
-                }
-                uint64_t fm[G];
-                int tot = 0;
-#pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    fm[g] = __ballot(old[g] == kUnseen);
-                    tot += __popcll(fm[g]);
-                }
-                if (tot) {
-                    int at = 0;
-                    if (lane == 0) at = atomicAdd(&ctl[0], tot);
-                    at = uniform(at);
-#pragma unroll
-                    for (int g = 0; g < G; ++g) {
-                        if ((fm[g] >> lane) & 1ull) q[at + lanes_below(fm[g])] = (uint16_t)r[g];
-                        at += __popcll(fm[g]);
-                    }
-                }
+                for (int g = 0; g < G; ++g)
+                    if (lv[g] == kUnseen) lvl[lds_swz(r[g])] = (uint32_t)(L + 1);
                 if (SYM && L > 0) {
-                    // next hop of each expanded y: lowest slot one level closer
+                    // next hop of each expanded y: the lowest slot one level
+                    // closer writes itself (mbcnt on the ballot)
 #pragma unroll
                     for (int g = 0; g < G; ++g) {
                         if (g < n) {
-                            const uint64_t m = __ballot(lv[g] == (uint32_t)(L - 1));
-                            if (m) {
-                                // readlane with every lane active: an operand the
-                                // compiler sinks into a lane-0-only block would
-                                // leave the other lanes' values unwritten
-                                const int sl = __ffsll((unsigned long long)m) - 1;
-                                const int y = read_lane(mine, g);
-                                const int nb = read_lane(r[g], sl);
-                                if (lane == 0) {
-                                    nhv[y] = (uint16_t)nb;
-                                    nhs[y] = (uint8_t)sl;
-                                }
+                            const bool cl = lv[g] == (uint32_t)(L - 1);
+                            const uint64_t m = __ballot(cl);
+                            if (cl && lanes_below(m) == 0) {
+                                const int y = q[base + g];
+                                nhv[y] = (uint16_t)r[g];
+                                nhs[y] = (uint8_t)lane;
                             }
                         }
                     }
                 }
             }
-            __syncthreads();                     // level L+1 complete
+            __syncthreads();                     // level L+1 marked
+            // ---- collect level L+1 in ascending vertex order: each wave
+            // counts its slice, then writes it after the lower slices
+            const int s0 = w * slice, s1 = min(V, s0 + slice);
+            int cnt = 0;
+            for (int x0 = s0; x0 < s1; x0 += 64) {
+                const int x = x0 + lane;
+                cnt += __popcll(__ballot(x < s1 && lvl[lds_swz(x)] == (uint32_t)(L + 1)));
+            }
+            if (lane == 0) ctl[w] = cnt;
+            __syncthreads();
+            int at = hi, total = 0;
+#pragma unroll
+            for (int k = 0; k < NW; ++k) {
+                const int c = ctl[k];
+                at += k < w ? c : 0;
+                total += c;
+            }
+            for (int x0 = s0; x0 < s1; x0 += 64) {
+                const int x = x0 + lane;
+                const bool hit = x < s1 && lvl[lds_swz(x)] == (uint32_t)(L + 1);
+                const uint64_t m = __ballot(hit);
+                if (hit) q[at + lanes_below(m)] = (uint16_t)x;
+                at += __popcll(m);
+            }
+            __syncthreads();                     // queue and counts consumed
             lo = hi;
-            hi = ctl[0];
-            __syncthreads();                     // every wave has read the tail
+            hi += total;
         }
 
         if (!SYM && want_nh) {
