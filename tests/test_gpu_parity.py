@@ -425,3 +425,70 @@ def test_ecmp_counts_match_dag_walk_dragonfly(ctx):
         for x in range(csr.V):
             seqs = shortest_paths_lex(csr.row_ptr, csr.col, dist[d], x, d)
             assert paths[d, x] == len(seqs)
+
+
+def _count_dp(csr, dist_row):
+    """Shortest-route counts toward one destination by the level DP, in
+    Python integers, saturated at 2**64-1 like the kernel."""
+    V = csr.V
+    order = sorted((int(dist_row[x]), x) for x in range(V) if dist_row[x] != 0xFFFF)
+    cnt = [0] * V
+    for dx, x in order:
+        if dx == 0:
+            cnt[x] = 1
+            continue
+        c = 0
+        for e in range(csr.row_ptr[x], csr.row_ptr[x + 1]):
+            n = int(csr.col[e])
+            if dist_row[n] != 0xFFFF and int(dist_row[n]) + 1 == dx:
+                c += cnt[n]
+        cnt[x] = c
+    return np.array([min(c, 2**64 - 1) for c in cnt], dtype=np.uint64)
+
+
+@pytest.mark.parametrize("case", ["fat_tree:8", "random", "ladder", "star"])
+def test_ecmp_counts_vs_level_dp(ctx, case):
+    """ECMP counts against a Python DP: ecmp_count_rows_kernel (64-wide rows)
+    including counts past 2**64 (a 70-rung ladder has 2**68 shortest routes
+    end to end: saturated), and the CSR kernel on a star of degree 130 (no
+    64-wide rows)."""
+    from sdnmpi_amd.topologies import CSR
+    if case == "fat_tree:8":
+        csr = T.by_name("fat_tree:8").csr()
+    elif case == "random":
+        rng = np.random.default_rng(7)
+        V = 300
+        adj = [sorted(set(rng.choice(V, size=rng.integers(1, 9), replace=False).tolist()) - {u})
+               for u in range(V)]
+        rp = np.concatenate([[0], np.cumsum([len(a) for a in adj])])
+        col = np.array([v for a in adj for v in a], np.int64)
+        csr = CSR(np.arange(1, V + 1), rp, col, np.concatenate([np.arange(1, len(a) + 1) for a in adj]))
+    elif case == "star":
+        V = 131                                  # hub 0 joined to 1..130, leaves 1-2 linked
+        nb = [list(range(1, V))] + [[0] for _ in range(1, V)]
+        nb[1].append(2)
+        nb[2].append(1)
+        rp = np.concatenate([[0], np.cumsum([len(a) for a in nb])])
+        col = np.array([v for a in nb for v in a], np.int64)
+        csr = CSR(np.arange(1, V + 1), rp, col, np.concatenate([np.arange(1, len(a) + 1) for a in nb]))
+    else:
+        R = 70                                   # rungs: vertices 2i, 2i+1
+        V = 2 * R
+        nb = [[] for _ in range(V)]
+        for i in range(R - 1):
+            for a in (2 * i, 2 * i + 1):
+                for b in (2 * i + 2, 2 * i + 3):
+                    nb[a].append(b)
+                    nb[b].append(a)
+        nb = [sorted(x) for x in nb]
+        rp = np.concatenate([[0], np.cumsum([len(a) for a in nb])])
+        col = np.array([v for a in nb for v in a], np.int64)
+        csr = CSR(np.arange(1, V + 1), rp, col, np.concatenate([np.arange(1, len(a) + 1) for a in nb]))
+    ctx.upload(csr)
+    dsts = np.arange(0, csr.V, 5 if case != "ladder" else 1, dtype=np.int32)
+    dist, _, _ = ctx.shortest_tables(dsts)
+    paths = ctx.ecmp_counts(dist)
+    for i in range(0, len(dsts), 3 if case != "ladder" else 7):
+        np.testing.assert_array_equal(paths[i], _count_dp(csr, dist[i]))
+    if case == "ladder":
+        assert int(paths[0, csr.V - 1]) == 2**64 - 1
