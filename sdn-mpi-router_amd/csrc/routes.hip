@@ -166,6 +166,76 @@ __global__ __launch_bounds__(256) void route_jump_kernel(
     }
 }
 
+// Packed form of the walk for V <= 65535 and 16-bit ports: the int32 trees
+// are first packed to parent | port << 16 (one 4-byte gather per entry
+// instead of two, half the cache footprint) and the 16th-ancestor table is
+// u16 (0xFFFF: none).
+__global__ __launch_bounds__(256) void tree_pack_kernel(size_t n, const int32_t *__restrict__ parent,
+                                                        const int32_t *__restrict__ port,
+                                                        uint32_t *__restrict__ tree,
+                                                        uint16_t *__restrict__ par16)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const int32_t p = parent[i];
+        tree[i] = p < 0 ? 0xFFFFFFFFu : ((uint32_t)p | ((uint32_t)port[i] & 0xFFFFu) << 16);
+        par16[i] = p < 0 ? (uint16_t)0xFFFFu : (uint16_t)p;
+    }
+}
+
+// out[r][v] = a[r][b[r][v]] on u16 ancestor tables (0xFFFF stays 0xFFFF)
+__global__ __launch_bounds__(256) void tree_compose16_kernel(int V, size_t n,
+                                                             const uint16_t *__restrict__ a,
+                                                             const uint16_t *__restrict__ b,
+                                                             uint16_t *__restrict__ out)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const uint16_t x = b[i];
+        out[i] = x == 0xFFFFu ? (uint16_t)0xFFFFu : a[(i / (size_t)V) * V + x];
+    }
+}
+
+struct Anc16 {
+    const uint16_t *a[5];    // a[j]: the 2^j-th ancestor (a[0] unused: tree)
+};
+
+template <int P>
+__global__ __launch_bounds__(256) void route_jump_packed_kernel(
+    int V, const uint32_t *__restrict__ tree, Anc16 anc,
+    const int32_t *__restrict__ rows, const int32_t *__restrict__ dsts,
+    const int32_t *__restrict__ last_port, int npairs, const int64_t *__restrict__ off,
+    int32_t *__restrict__ hop_switch, int32_t *__restrict__ hop_port)
+{
+    const int64_t nthr = (int64_t)npairs * P;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nthr;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int i = (int)(t / P), k = (int)(t % P);
+        const int64_t lo = off[i], hi = off[i + 1];
+        if (hi <= lo) continue;               // unreachable: no entries
+        const int64_t h = hi - lo - 1;        // hops; entry h is the destination
+        const size_t rb = (size_t)rows[i] * V;
+        int y = dsts[i];
+        if (k == 0) {
+            hop_switch[lo + h] = y;
+            hop_port[lo + h] = last_port[i];
+        }
+        if (k >= h) continue;
+        // k-th ancestor by binary jumps: popcount(k) dependent loads
+        if (k & 1) y = (int)(tree[rb + y] & 0xFFFFu);
+#pragma unroll
+        for (int j = 1; (1 << j) < P; ++j)
+            if (k & (1 << j)) y = anc.a[j][rb + y];
+        const uint16_t *__restrict__ ancP = anc.a[__builtin_ctz(P)];
+        for (int64_t u = k; u < h; u += P) {
+            const uint32_t e = tree[rb + y];
+            hop_switch[lo + h - u - 1] = (int32_t)(e & 0xFFFFu);
+            hop_port[lo + h - u - 1] = (int32_t)(e >> 16);
+            if (u + P < h) y = ancP[rb + y];
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void route_walk_kernel(
     int V, const int32_t *__restrict__ parent, const int32_t *__restrict__ port,
     const int32_t *__restrict__ rows, const int32_t *__restrict__ dsts,
@@ -232,13 +302,36 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
     const size_t n = (size_t)nrows * (size_t)ctx->V;
     int32_t *anc = nullptr, *tmp = nullptr;
     if (!serial) {
-        int rc = sdnr_reserve(&ctx->scratch2, &ctx->scratch2_bytes, 2 * n * sizeof(int32_t) + 64);
+        int rc = sdnr_reserve(&ctx->scratch2, &ctx->scratch2_bytes, 14 * n + 64);
         if (rc) return rc;
         anc = static_cast<int32_t *>(ctx->scratch2);
         tmp = anc + n;
     }
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
-    if (serial) {
+    const char *pk = getenv("SDNROUTE_ROUTE_PACKED");          // "0": int32 tables
+    const bool packed = !serial && ctx->V <= 0xFFFF && ctx->port16 && !(pk && !strcmp(pk, "0"));
+    if (packed) {
+        // scratch2 (14n bytes): tree u32 [n] | u16 ancestor tables a1..a16 [n]
+        uint32_t *tree = reinterpret_cast<uint32_t *>(anc);
+        uint16_t *a16 = reinterpret_cast<uint16_t *>(tree + n);
+        const int cg = ctx->num_cus * 8;
+        hipLaunchKernelGGL(tree_pack_kernel, dim3(cg), dim3(256), 0, ctx->stream, n, d_parent,
+                           d_port, tree, a16);
+        Anc16 tabs{};
+        for (int j = 1; j <= 4; ++j) {
+            uint16_t *o = a16 + (size_t)j * n;
+            const uint16_t *prev = a16 + (size_t)(j - 1) * n;
+            hipLaunchKernelGGL(tree_compose16_kernel, dim3(cg), dim3(256), 0, ctx->stream,
+                               ctx->V, n, prev, prev, o);
+            tabs.a[j] = o;
+        }
+        int64_t g = ((int64_t)npairs * 16 + 255) / 256;
+        if (g > ctx->num_cus * 16) g = ctx->num_cus * 16;
+        ctx->last_kernel = "route_jump_packed_kernel<16>";
+        hipLaunchKernelGGL(route_jump_packed_kernel<16>, dim3((unsigned)g), dim3(256), 0,
+                           ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts, d_last_port, npairs,
+                           d_off, d_switch, d_hport);
+    } else if (serial) {
         int g = (npairs + 255) / 256;
         if (g > ctx->num_cus * 16) g = ctx->num_cus * 16;
         ctx->last_kernel = "route_walk_kernel";

@@ -293,7 +293,7 @@ def test_route_entries_batched_fake_engine():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("walk", ["auto", "serial", "p4", "p8"])
+@pytest.mark.parametrize("walk", ["auto", "serial", "int32", "p4", "p8"])
 @pytest.mark.parametrize("name", ["mock", "fat_tree_k8", "dragonfly_a4_h2_p2", "random_V40",
                                   "torus_5x3x2"])
 def test_route_entries_match_reference(monkeypatch, name, walk):
@@ -302,8 +302,10 @@ def test_route_entries_match_reference(monkeypatch, name, walk):
     from oracle import oracle as O
     if walk == "serial":
         monkeypatch.setenv("SDNROUTE_ROUTE_WALK", walk)
-    elif walk != "auto":
-        monkeypatch.setenv("SDNROUTE_ROUTE_P", walk[1:])
+    elif walk != "auto":                         # int32-table jump kernels
+        monkeypatch.setenv("SDNROUTE_ROUTE_PACKED", "0")
+        if walk != "int32":
+            monkeypatch.setenv("SDNROUTE_ROUTE_P", walk[1:])
     g = G.Golden(name)
     fabric = g.fabric()
     db = fabric.populate(TopologyDB())
