@@ -16,8 +16,11 @@
 // 16 lanes with a 16th-ancestor table (four compositions of the parent
 // table), so the lanes of a pair store 16 consecutive entries per step and a
 // path of h hops costs ~k + h/16 dependent loads (k < 16: the lane's start);
-// route_walk_kernel (one lane per pair, SDNROUTE_ROUTE_WALK=serial) is the
-// plain form.  The tree rows stay L2 / Infinity-Cache resident; the output is
+// route_jump_packed_kernel<16> (the default when V <= 65535 and ports are
+// 16-bit) walks a packed copy of the trees (parent | port << 16: one gather
+// per entry) with u16 2^j-th-ancestor tables, so lane k reaches its start in
+// popcount(k) loads; route_walk_kernel (one lane per pair,
+// SDNROUTE_ROUTE_WALK=serial) is the plain form.  The tree rows stay L2 / Infinity-Cache resident; the output is
 // written once.
 #include <stdlib.h>
 #include <string.h>
