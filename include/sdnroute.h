@@ -161,7 +161,7 @@ int sdnr_ecmp_routes(sdnr_ctx *ctx, const uint16_t *dist, const uint64_t *paths,
  *   last entry is (dsts[i], last_port[i]).  Bit-identical to find_route's
  *   fdb with switch ids mapped to dpids.
  * nrows is required in both modes (the expansion builds ancestor
- * table of the nrows trees).  Host buffers: the tables are staged per call
+ * tables of the nrows trees).  Host buffers: the tables are staged per call
  * (nrows * V entries each). */
 int sdnr_route_offsets(sdnr_ctx *ctx, const int32_t *hops, int32_t nrows,
                        const int32_t *rows, const int32_t *dsts, int32_t npairs,
