@@ -471,6 +471,8 @@ def main():
     value = routes / (ms_per_step / 1e3)
     bytes_launch = algorithmic_bytes_per_source(V, E, args.mode, packed) * (hi - lo)
     achieved = bytes_launch / (kern_ms / 1e3) / 1e9
+    per_entry = (4 if packed else 8) if args.mode == "dfs" else 10
+    compulsory = 4 * (V + 1) + 8 * E + per_entry * V * (hi - lo)
     traffic = None
     layout = "packed" if packed else ("int32" if args.mode == "dfs" else "u16+int32")
     if os.path.exists(TRAFFIC_FILE):
@@ -508,6 +510,10 @@ def main():
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "kernel": ctx.last_kernel(),
             "kernel_ms": kern_ms, "bytes_per_launch": bytes_launch,
+            # the compulsory bytes -- CSR (row_ptr, col,
+            # port) read once + this launch's tables written once
+            "compulsory_bytes": compulsory,
+            "compulsory_gbs": compulsory / (kern_ms / 1e3) / 1e9,
         },
         "switch_pair_routes_per_s": float(S) * V / (ms_per_step / 1e3),
         "teps": float(hi - lo) * E / (kern_ms / 1e3),

@@ -125,8 +125,9 @@ int sdnr_shortest_tables(sdnr_ctx *ctx, const int32_t *dst, int32_t ndst,
                          uint16_t *dist, int32_t *nh, int32_t *nh_port,
                          uint32_t flags);
 
-/* All-pairs hop distances by blocked min-plus (Floyd-Warshall) closure for
- * small dense graphs: dist[i*V+j] = hops i -> j (SDNR_DIST_INF if none).
+/* All-pairs hop distances by min-plus squaring (D <- min(D, D (x) D) until
+ * stable) for small dense graphs: dist[i*V+j] = hops i -> j (SDNR_DIST_INF
+ * if none).
  * V <= 16384. */
 int sdnr_apsp(sdnr_ctx *ctx, uint16_t *dist, uint32_t flags);
 
