@@ -244,6 +244,7 @@ int sdnr_graph_upload(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_pt
     // kernels: padding and the extra row V hold the sentinel vertex V; the
     // in-neighbour rows (same layout) and packed out-degrees feed the
     // counted-pop kernel
+    int32_t max_indeg = 0x7FFFFFFF;             // known only with the u16 rows
     if (V < 65535 && maxdeg <= SDNR_WAVE) {
         const size_t rows = ((size_t)V + 1) * SDNR_WAVE;
         std::vector<uint16_t> a16(rows, (uint16_t)V), r16(rows, (uint16_t)V);
@@ -259,6 +260,7 @@ int sdnr_graph_upload(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_pt
         }
         int32_t maxin = 0;
         for (int32_t v = 0; v < V; ++v) maxin = indeg[v] > maxin ? indeg[v] : maxin;
+        max_indeg = maxin;
         bool sym = true;
         if (maxin <= SDNR_WAVE) {
             std::vector<int32_t> fill((size_t)V, 0);
@@ -314,6 +316,7 @@ int sdnr_graph_upload(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_pt
     ctx->E = E;
     ctx->W = W;
     ctx->max_deg = maxdeg;
+    ctx->max_indeg = max_indeg;
     ctx->port16 = port16;
     ctx->symmetric = symmetric;
     return SDNR_OK;

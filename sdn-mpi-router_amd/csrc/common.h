@@ -49,6 +49,7 @@ struct sdnr_ctx {
 
     // graph (device)
     int32_t V = -1, E = 0, max_deg = 0;
+    int32_t max_indeg = 0x7FFFFFFF;     // maximum in-degree (set with adj16/radj16)
     int32_t W = 0;                      // ELL row width (0: CSR only)
     int32_t *row_ptr = nullptr, *col = nullptr, *port = nullptr;
     int32_t *ell_col = nullptr, *ell_port = nullptr;

@@ -418,9 +418,180 @@ __global__ __launch_bounds__(NW * 64) void bfs_dest_kernel(
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// bfs_dest_lanes_kernel<LPR,NW,G,SYM>: the per-destination BFS for graphs too
+// large for bfs_dest_kernel's LDS image (torus 32^3: V = 32,768) with rows of
+// at most LPR <= 32 entries.  One workgroup per destination, all of its LDS:
+// levels u16 [V+1], the BFS queue u16 [V], a claim bitmap [V+1 bits].  A row
+// needs only LPR lanes, so one wave instruction expands R = 64/LPR frontier
+// vertices (lane -> row sub = lane/LPR, slot pos = lane%LPR), G such groups
+// in flight per wave.  An unseen neighbour is claimed with an LDS atomicOr on
+// its bit (exactly one claimant), which sets its level and appends it (one
+// queue-tail atomic per wave-iteration).  On a symmetric graph the row of a
+// level-L vertex is also its out-row and its level-(L-1) entries are final,
+// so its next hop -- the lowest such slot -- is stored straight to the table
+// during the expansion; asymmetric graphs take one pass over the out-rows at
+// the end.  Distances are written once from LDS, coalesced.
+// ---------------------------------------------------------------------------
+__host__ __device__ inline size_t bfs_lanes_words(int V)
+{
+    const size_t LW = ((size_t)(V + 2) / 2 + 3) & ~(size_t)3;   // u16 levels, V+1
+    const size_t QW = ((size_t)(V + 1) / 2 + 3) & ~(size_t)3;   // u16 queue
+    const size_t BW = (((size_t)V + 1 + 31) / 32 + 3) & ~(size_t)3;
+    return LW + QW + BW + 4;
+}
+
+template <int LPR, int NW, int G, bool SYM>
+__global__ __launch_bounds__(NW * 64) void bfs_dest_lanes_kernel(
+    int V, int W, const uint16_t *__restrict__ adj, const uint16_t *__restrict__ radj,
+    const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ port,
+    const int32_t *__restrict__ ell_port, const int32_t *__restrict__ dst, int ndst,
+    uint16_t *__restrict__ out_dist, int32_t *__restrict__ out_nh,
+    int32_t *__restrict__ out_nh_port)
+{
+    constexpr int R = 64 / LPR;
+    constexpr uint16_t kUn = 0xFFFFu, kSent = 0xFFFEu;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int LW = (int)((((size_t)V + 2) / 2 + 3) & ~(size_t)3);
+    const int QW = (int)((((size_t)V + 1) / 2 + 3) & ~(size_t)3);
+    const int BW = (int)((((size_t)V + 1 + 31) / 32 + 3) & ~(size_t)3);
+    uint16_t *lvl = reinterpret_cast<uint16_t *>(lds);
+    uint16_t *q = reinterpret_cast<uint16_t *>(lds + LW);
+    uint32_t *claim = lds + LW + QW;
+    int *ctl = reinterpret_cast<int *>(claim + BW);     // [0] queue tail
+    const uint16_t *inrow = SYM ? adj : radj;
+    const int lane = lane_id();
+    const int w = uniform((int)(threadIdx.x >> 6));
+    const int sub = lane / LPR, pos = lane % LPR;
+    const uint64_t grp = (LPR == 64 ? ~0ull : ((1ull << LPR) - 1ull)) << (sub * LPR);
+    const bool want_nh = out_nh != nullptr;
+
+    for (int di = blockIdx.x; di < ndst; di += gridDim.x) {
+        const int d = uniform(dst[di]);
+        uint16_t *drow = out_dist + (size_t)di * V;
+        int32_t *hrow = want_nh ? out_nh + (size_t)di * V : nullptr;
+        int32_t *prow = want_nh ? out_nh_port + (size_t)di * V : nullptr;
+        if (d < 0 || d >= V) {                   // unknown destination: empty row
+            for (int v = threadIdx.x; v < V; v += blockDim.x) {
+                drow[v] = kUn;
+                if (want_nh) {
+                    hrow[v] = -1;
+                    prow[v] = -1;
+                }
+            }
+            continue;
+        }
+        for (int i = threadIdx.x; i <= V; i += blockDim.x)
+            lvl[i] = i == d ? (uint16_t)0 : (i == V ? kSent : kUn);
+        for (int i = threadIdx.x; i < BW; i += blockDim.x) claim[i] = 0u;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            claim[d >> 5] |= 1u << (d & 31);
+            claim[V >> 5] |= 1u << (V & 31);
+            q[0] = (uint16_t)d;
+            ctl[0] = 1;
+        }
+        __syncthreads();
+
+        int lo = 0, hi = 1;
+        for (int L = 0; lo < hi; ++L) {
+            for (int base = lo + w * (R * G); base < hi; base += NW * R * G) {
+                int y[G], r[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const int idx = base + g * R + sub;
+                    y[g] = idx < hi ? (int)q[idx] : V;         // past hi: sentinel row
+                }
+#pragma unroll
+                for (int g = 0; g < G; ++g) r[g] = inrow[(size_t)y[g] * 64 + pos];
+                uint32_t lv[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) lv[g] = lvl[r[g]];
+                bool won[G];
+                int nwon = 0;
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    won[g] = false;
+                    if (lv[g] == kUn) {
+                        const uint32_t b = 1u << (r[g] & 31);
+                        won[g] = (atomicOr(&claim[r[g] >> 5], b) & b) == 0u;
+                    }
+                    nwon += __popcll(__ballot(won[g]));
+                }
+                if (nwon) {
+                    int at = 0;
+                    if (lane == 0) at = atomicAdd(&ctl[0], nwon);
+                    at = read_lane(at, 0);
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        const uint64_t m = __ballot(won[g]);
+                        if (won[g]) {
+                            lvl[r[g]] = (uint16_t)(L + 1);
+                            q[at + lanes_below(m)] = (uint16_t)r[g];
+                        }
+                        at += __popcll(m);
+                    }
+                }
+                if (SYM && want_nh && L > 0) {
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        const bool cl = lv[g] == (uint32_t)(L - 1);
+                        const uint64_t m = __ballot(cl) & grp;
+                        if (cl && lanes_below(m) == 0 && y[g] < V) {
+                            const int yy = y[g];
+                            hrow[yy] = r[g];
+                            prow[yy] = W > 0 ? ell_port[(size_t)yy * W + pos]
+                                             : port[row_ptr[yy] + pos];
+                        }
+                    }
+                }
+            }
+            __syncthreads();                     // level L+1 claimed and queued
+            lo = hi;
+            hi = ctl[0];
+            __syncthreads();                     // every wave has read the tail
+        }
+
+        if (!SYM && want_nh) {
+            // next hop over the out-rows: lowest slot whose level is one less
+            for (int base = w * (R * G); base < V; base += NW * R * G) {
+                int r[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const int v = base + g * R + sub;
+                    r[g] = adj[(size_t)(v < V ? v : V) * 64 + pos];
+                }
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const int v = base + g * R + sub;
+                    const uint32_t lx = v < V ? lvl[v] : kUn;
+                    const bool cl = lx != kUn && lx != 0u && (uint32_t)lvl[r[g]] + 1u == lx;
+                    const uint64_t m = __ballot(cl) & grp;
+                    if (cl && lanes_below(m) == 0) {
+                        hrow[v] = r[g];
+                        prow[v] = W > 0 ? ell_port[(size_t)v * W + pos] : port[row_ptr[v] + pos];
+                    }
+                }
+            }
+        }
+
+        // distances once, coalesced; no next hop for d and unreached vertices
+        for (int v = threadIdx.x; v < V; v += blockDim.x) {
+            const uint16_t lx = lvl[v];
+            drow[v] = lx;
+            if (want_nh && (lx == kUn || lx == 0)) {
+                hrow[v] = -1;
+                prow[v] = -1;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
-// SDNROUTE_SP_STRATEGY=msbfs|dest forces the shortest-mode kernel (tests)
+// SDNROUTE_SP_STRATEGY=msbfs|lanes forces the shortest-mode kernel (tests)
 static const char *sp_strategy()
 {
     const char *f = getenv("SDNROUTE_SP_STRATEGY");
@@ -438,7 +609,7 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
     const bool dest_ok = ctx->adj16 != nullptr && ctx->radj16 != nullptr && V < 65534 &&
                          dlds <= 64 * 1024;
     const char *force = sp_strategy();
-    if (dest_ok && strcmp(force, "msbfs") != 0) {
+    if (dest_ok && strcmp(force, "msbfs") != 0 && strcmp(force, "lanes") != 0) {
         const bool sym = ctx->radj16 == ctx->adj16;
         size_t bpc = SDNR_LDS_PER_CU / dlds;
         if (bpc > 8) bpc = 8;
@@ -469,6 +640,58 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
             if (sym) SDNR_BFS_DEST(4, 16, true); else SDNR_BFS_DEST(4, 16, false);
         }
 #undef SDNR_BFS_DEST
+        SDNR_HIP(hipGetLastError());
+        if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+        return SDNR_OK;
+    }
+    // lane-packed per-destination BFS: rows of <= 32 entries, one workgroup's
+    // LDS holds the levels, queue and claim bits
+    const int maxrow = ctx->max_deg > ctx->max_indeg ? ctx->max_deg : ctx->max_indeg;
+    const size_t llds = bfs_lanes_words(V) * 4;
+    const bool lanes_ok = ctx->adj16 != nullptr && ctx->radj16 != nullptr && V < 65534 &&
+                          maxrow <= 32 && llds <= SDNR_MAX_LDS_PER_BLOCK - 1024;
+    if (lanes_ok && strcmp(force, "msbfs") != 0) {
+        const bool sym = ctx->radj16 == ctx->adj16;
+        size_t bpc = SDNR_LDS_PER_CU / llds;
+        if (bpc > 2) bpc = 2;
+        if (bpc < 1) bpc = 1;
+        int grid = (int)((size_t)ctx->num_cus * bpc);
+        if (grid > ndst) grid = ndst;
+        static const char *names[2][4] = {
+            {"bfs_dest_lanes_kernel<4,asym>", "bfs_dest_lanes_kernel<8,asym>",
+             "bfs_dest_lanes_kernel<16,asym>", "bfs_dest_lanes_kernel<32,asym>"},
+            {"bfs_dest_lanes_kernel<4,sym>", "bfs_dest_lanes_kernel<8,sym>",
+             "bfs_dest_lanes_kernel<16,sym>", "bfs_dest_lanes_kernel<32,sym>"}};
+        const int li = maxrow <= 4 ? 0 : maxrow <= 8 ? 1 : maxrow <= 16 ? 2 : 3;
+        ctx->last_kernel = names[sym ? 1 : 0][li];
+        // SDNROUTE_SP_LANES_G=2|4|8: frontier groups in flight per wave (tuning)
+        const char *gf = getenv("SDNROUTE_SP_LANES_G");
+        const int gsel = gf ? atoi(gf) : 8;
+#define SDNR_BFS_LANES_G(LPR_, S_, G_)                                                       \
+    do {                                                                                     \
+        auto k = bfs_dest_lanes_kernel<LPR_, 16, G_, S_>;                                    \
+        sdnr_allow_lds(reinterpret_cast<const void *>(k), llds);                             \
+        hipLaunchKernelGGL(k, dim3(grid), dim3(16 * 64), llds, ctx->stream, V, ctx->W,       \
+                           ctx->adj16, ctx->radj16, ctx->row_ptr, ctx->port, ctx->ell_port,  \
+                           d_dst, ndst, d_dist, d_nh, d_nh_port);                            \
+    } while (0)
+#define SDNR_BFS_LANES(LPR_, S_)                                                             \
+    do {                                                                                     \
+        if (gsel == 2) SDNR_BFS_LANES_G(LPR_, S_, 2);                                        \
+        else if (gsel == 4) SDNR_BFS_LANES_G(LPR_, S_, 4);                                   \
+        else SDNR_BFS_LANES_G(LPR_, S_, 8);                                                  \
+    } while (0)
+#define SDNR_BFS_LANES_S(LPR_)                                                               \
+    do {                                                                                     \
+        if (sym) SDNR_BFS_LANES(LPR_, true); else SDNR_BFS_LANES(LPR_, false);               \
+    } while (0)
+        if (li == 0) SDNR_BFS_LANES_S(4);
+        else if (li == 1) SDNR_BFS_LANES_S(8);
+        else if (li == 2) SDNR_BFS_LANES_S(16);
+        else SDNR_BFS_LANES_S(32);
+#undef SDNR_BFS_LANES_S
+#undef SDNR_BFS_LANES
+#undef SDNR_BFS_LANES_G
         SDNR_HIP(hipGetLastError());
         if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
         return SDNR_OK;

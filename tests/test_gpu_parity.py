@@ -177,7 +177,7 @@ def test_dfs_fullsize_tree_properties(ctx):
             assert k < hi and csr.col[k] == v and csr.port[k] == t[s, v]
 
 
-@pytest.mark.parametrize("strategy", ["auto", "msbfs"])
+@pytest.mark.parametrize("strategy", ["auto", "msbfs", "lanes"])
 @pytest.mark.parametrize("name", G.SMALL)
 def test_shortest_small_all_destinations(ctx, monkeypatch, name, strategy):
     if strategy != "auto":
@@ -231,14 +231,19 @@ def test_shortest_fullsize_fat_tree(ctx, monkeypatch, strategy):
     np.testing.assert_array_equal(nhp, nhpo)
 
 
-def test_shortest_fullsize_torus_sample(ctx):
-    """torus 32^3 (the BASELINE multi-source BFS config), spread destinations."""
+@pytest.mark.parametrize("strategy", ["auto", "msbfs"])
+def test_shortest_fullsize_torus_sample(ctx, monkeypatch, strategy):
+    """torus 32^3 (the BASELINE multi-source BFS config), spread destinations:
+    the lane-packed per-destination BFS and the 64-destination bitset BFS."""
+    if strategy != "auto":
+        monkeypatch.setenv("SDNROUTE_SP_STRATEGY", strategy)
     fabric = T.torus3d(32, 32, 32)
     csr = fabric.csr()
     dsts = np.linspace(0, csr.V - 1, 96).astype(np.int32)
     ctx.upload(csr)
     dist, nh, nhp = ctx.shortest_tables(dsts)
-    assert ctx.last_kernel().startswith("msbfs_level_kernel")
+    assert ctx.last_kernel().startswith(
+        "bfs_dest_lanes_kernel<8,sym>" if strategy == "auto" else "msbfs_level_kernel")
     do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
     np.testing.assert_array_equal(dist, do)
     np.testing.assert_array_equal(nh, nho)
