@@ -422,50 +422,82 @@ __global__ __launch_bounds__(NW * 64) void bfs_dest_kernel(
 // ---------------------------------------------------------------------------
 // bfs_dest_lanes_kernel<LPR,NW,G,SYM>: the per-destination BFS for graphs too
 // large for bfs_dest_kernel's LDS image (torus 32^3: V = 32,768) with rows of
-// at most LPR <= 32 entries.  One workgroup per destination, all of its LDS:
-// levels u16 [V+1], the BFS queue u16 [V], a claim bitmap [V+1 bits].  A row
-// needs only LPR lanes, so one wave instruction expands R = 64/LPR frontier
-// vertices (lane -> row sub = lane/LPR, slot pos = lane%LPR), G such groups
-// in flight per wave.  An unseen neighbour is claimed with an LDS atomicOr on
-// its bit (exactly one claimant), which sets its level and appends it (one
-// queue-tail atomic per wave-iteration).  On a symmetric graph the row of a
-// level-L vertex is also its out-row and its level-(L-1) entries are final,
-// so its next hop -- the lowest such slot -- is stored straight to the table
-// during the expansion; asymmetric graphs take one pass over the out-rows at
-// the end.  Distances are written once from LDS, coalesced.
+// at most LPR <= 32 entries.  One workgroup per destination; LDS holds the
+// levels (u16), the BFS queue (u16), a claim bitmap and the next-hop row slot
+// of every vertex (4 bits if LPR <= 8, else 8).
+//  * A row needs only LPR lanes, so one wave instruction expands R = 64/LPR
+//    frontier vertices (lane -> row sub = lane/LPR, slot pos = lane%LPR), G
+//    such groups in flight per wave.  Symmetric graphs read the compact ELL
+//    rows (L2-resident: torus 786 KB instead of 4 MB of 64-wide rows).
+//  * An unseen neighbour is claimed with an LDS atomicOr on its bit (exactly
+//    one claimant), which sets its level and appends it to the queue (one
+//    tail atomic per wave-iteration).
+//  * On a symmetric graph the row of a level-L vertex is also its out-row
+//    and its level-(L-1) entries are final, so its next hop's slot (the
+//    lowest such lane of its group) goes to LDS during the expansion;
+//    asymmetric graphs take one pass over the out-rows at the end.
+//  * The tables are written once, coalesced: distances from LDS, next hop
+//    and port as the row entries at the stored slot.  (Storing the next hops
+//    straight to the tables in BFS order scattered 4-byte stores over the
+//    rows: 7x write amplification, 185 GB of HBM traffic on the torus.)
 // ---------------------------------------------------------------------------
-__host__ __device__ inline size_t bfs_lanes_words(int V)
+__host__ __device__ constexpr bool lanes_nibble(int LPR) { return LPR <= 8; }
+
+__host__ __device__ inline size_t bfs_lanes_bytes(int V, int LPR)
 {
-    const size_t LW = ((size_t)(V + 2) / 2 + 3) & ~(size_t)3;   // u16 levels, V+1
-    const size_t QW = ((size_t)(V + 1) / 2 + 3) & ~(size_t)3;   // u16 queue
-    const size_t BW = (((size_t)V + 1 + 31) / 32 + 3) & ~(size_t)3;
-    return LW + QW + BW + 4;
+    const size_t lv = (((size_t)V + 1) * 2 + 15) & ~(size_t)15;           // u16 levels [V+1]
+    const size_t qb = ((size_t)V * 2 + 15) & ~(size_t)15;                 // u16 queue [V]
+    const size_t cb = ((((size_t)V + 1 + 31) / 32) * 4 + 15) & ~(size_t)15;   // claim bits
+    const size_t sb = lanes_nibble(LPR) ? ((((size_t)V + 7) / 8) * 4 + 15) & ~(size_t)15
+                                        : ((((size_t)V + 3) / 4) * 4 + 15) & ~(size_t)15;
+    return lv + qb + cb + sb + 16;
 }
 
 template <int LPR, int NW, int G, bool SYM>
 __global__ __launch_bounds__(NW * 64) void bfs_dest_lanes_kernel(
     int V, int W, const uint16_t *__restrict__ adj, const uint16_t *__restrict__ radj,
-    const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ port,
+    const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+    const int32_t *__restrict__ port, const int32_t *__restrict__ ell_col,
     const int32_t *__restrict__ ell_port, const int32_t *__restrict__ dst, int ndst,
     uint16_t *__restrict__ out_dist, int32_t *__restrict__ out_nh,
     int32_t *__restrict__ out_nh_port)
 {
     constexpr int R = 64 / LPR;
+    constexpr bool NIB = lanes_nibble(LPR);
+    constexpr int SBITS = NIB ? 4 : 8, SPW = 32 / SBITS;       // slot bits, slots per word
+    constexpr uint32_t SNONE = NIB ? 0xFu : 0xFFu;
     constexpr uint16_t kUn = 0xFFFFu, kSent = 0xFFFEu;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const int LW = (int)((((size_t)V + 2) / 2 + 3) & ~(size_t)3);
-    const int QW = (int)((((size_t)V + 1) / 2 + 3) & ~(size_t)3);
-    const int BW = (int)((((size_t)V + 1 + 31) / 32 + 3) & ~(size_t)3);
-    uint16_t *lvl = reinterpret_cast<uint16_t *>(lds);
-    uint16_t *q = reinterpret_cast<uint16_t *>(lds + LW);
-    uint32_t *claim = lds + LW + QW;
-    int *ctl = reinterpret_cast<int *>(claim + BW);     // [0] queue tail
-    const uint16_t *inrow = SYM ? adj : radj;
+    const size_t lvb = (((size_t)V + 1) * 2 + 15) & ~(size_t)15;
+    const size_t qbb = ((size_t)V * 2 + 15) & ~(size_t)15;
+    const size_t cbb = ((((size_t)V + 1 + 31) / 32) * 4 + 15) & ~(size_t)15;
+    const int SW = (V + SPW - 1) / SPW;                         // slot words
+    uint8_t *base8 = reinterpret_cast<uint8_t *>(lds);
+    uint16_t *lvl = reinterpret_cast<uint16_t *>(base8);
+    uint16_t *q = reinterpret_cast<uint16_t *>(base8 + lvb);
+    uint32_t *claim = reinterpret_cast<uint32_t *>(base8 + lvb + qbb);
+    uint32_t *slotw = reinterpret_cast<uint32_t *>(base8 + lvb + qbb + cbb);
+    int *ctl = reinterpret_cast<int *>(slotw + ((SW + 3) & ~3));     // [0] queue tail
+    const int CW = (V + 1 + 31) / 32;
     const int lane = lane_id();
     const int w = uniform((int)(threadIdx.x >> 6));
     const int sub = lane / LPR, pos = lane % LPR;
-    const uint64_t grp = (LPR == 64 ? ~0ull : ((1ull << LPR) - 1ull)) << (sub * LPR);
+    const uint64_t grp = ((1ull << LPR) - 1ull) << (sub * LPR);
     const bool want_nh = out_nh != nullptr;
+    const bool ell = SYM && W > 0;
+
+    // row entry pos of vertex y (y == V: the sentinel row); padding -> V
+    auto row_in = [&](int y) -> int {
+        if (ell) {
+            const int e = (pos < W && y < V) ? ell_col[(size_t)y * W + pos] : -1;
+            return e < 0 ? V : e;
+        }
+        return (int)(SYM ? adj : radj)[(size_t)y * 64 + pos];
+    };
+    auto set_slot = [&](int y, int sl) {     // slot of y: clear the bits not in sl
+        const int sh = (y % SPW) * SBITS;
+        atomicAnd(&slotw[y / SPW], ~((SNONE & ~(uint32_t)sl) << sh));
+    };
 
     for (int di = blockIdx.x; di < ndst; di += gridDim.x) {
         const int d = uniform(dst[di]);
@@ -484,7 +516,8 @@ __global__ __launch_bounds__(NW * 64) void bfs_dest_lanes_kernel(
         }
         for (int i = threadIdx.x; i <= V; i += blockDim.x)
             lvl[i] = i == d ? (uint16_t)0 : (i == V ? kSent : kUn);
-        for (int i = threadIdx.x; i < BW; i += blockDim.x) claim[i] = 0u;
+        for (int i = threadIdx.x; i < CW; i += blockDim.x) claim[i] = 0u;
+        for (int i = threadIdx.x; i < SW; i += blockDim.x) slotw[i] = 0xFFFFFFFFu;
         __syncthreads();
         if (threadIdx.x == 0) {
             claim[d >> 5] |= 1u << (d & 31);
@@ -504,7 +537,7 @@ __global__ __launch_bounds__(NW * 64) void bfs_dest_lanes_kernel(
                     y[g] = idx < hi ? (int)q[idx] : V;         // past hi: sentinel row
                 }
 #pragma unroll
-                for (int g = 0; g < G; ++g) r[g] = inrow[(size_t)y[g] * 64 + pos];
+                for (int g = 0; g < G; ++g) r[g] = row_in(y[g]);
                 uint32_t lv[G];
 #pragma unroll
                 for (int g = 0; g < G; ++g) lv[g] = lvl[r[g]];
@@ -514,8 +547,8 @@ __global__ __launch_bounds__(NW * 64) void bfs_dest_lanes_kernel(
                 for (int g = 0; g < G; ++g) {
                     won[g] = false;
                     if (lv[g] == kUn) {
-                        const uint32_t b = 1u << (r[g] & 31);
-                        won[g] = (atomicOr(&claim[r[g] >> 5], b) & b) == 0u;
+                        const uint32_t bit = 1u << (r[g] & 31);
+                        won[g] = (atomicOr(&claim[r[g] >> 5], bit) & bit) == 0u;
                     }
                     nwon += __popcll(__ballot(won[g]));
                 }
@@ -538,12 +571,7 @@ __global__ __launch_bounds__(NW * 64) void bfs_dest_lanes_kernel(
                     for (int g = 0; g < G; ++g) {
                         const bool cl = lv[g] == (uint32_t)(L - 1);
                         const uint64_t m = __ballot(cl) & grp;
-                        if (cl && lanes_below(m) == 0 && y[g] < V) {
-                            const int yy = y[g];
-                            hrow[yy] = r[g];
-                            prow[yy] = W > 0 ? ell_port[(size_t)yy * W + pos]
-                                             : port[row_ptr[yy] + pos];
-                        }
+                        if (cl && lanes_below(m) == 0 && y[g] < V) set_slot(y[g], pos);
                     }
                 }
             }
@@ -560,7 +588,12 @@ __global__ __launch_bounds__(NW * 64) void bfs_dest_lanes_kernel(
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
                     const int v = base + g * R + sub;
-                    r[g] = adj[(size_t)(v < V ? v : V) * 64 + pos];
+                    if (W > 0) {
+                        const int e = (pos < W && v < V) ? ell_col[(size_t)v * W + pos] : -1;
+                        r[g] = e < 0 ? V : e;
+                    } else {
+                        r[g] = adj[(size_t)(v < V ? v : V) * 64 + pos];
+                    }
                 }
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
@@ -568,21 +601,48 @@ __global__ __launch_bounds__(NW * 64) void bfs_dest_lanes_kernel(
                     const uint32_t lx = v < V ? lvl[v] : kUn;
                     const bool cl = lx != kUn && lx != 0u && (uint32_t)lvl[r[g]] + 1u == lx;
                     const uint64_t m = __ballot(cl) & grp;
-                    if (cl && lanes_below(m) == 0) {
-                        hrow[v] = r[g];
-                        prow[v] = W > 0 ? ell_port[(size_t)v * W + pos] : port[row_ptr[v] + pos];
-                    }
+                    if (cl && lanes_below(m) == 0) set_slot(v, pos);
                 }
             }
+            __syncthreads();
         }
 
-        // distances once, coalesced; no next hop for d and unreached vertices
-        for (int v = threadIdx.x; v < V; v += blockDim.x) {
-            const uint16_t lx = lvl[v];
-            drow[v] = lx;
-            if (want_nh && (lx == kUn || lx == 0)) {
-                hrow[v] = -1;
-                prow[v] = -1;
+        // tables once, coalesced; the next hop and its port are the row
+        // entries at the stored slot (U vertices per thread, loads in flight
+        // together)
+        constexpr int U = 4;
+        for (int v0 = threadIdx.x; v0 < V; v0 += U * (int)blockDim.x) {
+            int h[U], pt[U], e[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int v = v0 + k * (int)blockDim.x;
+                e[k] = -1;
+                if (v < V) {
+                    const uint16_t lx = lvl[v];
+                    drow[v] = lx;
+                    const uint32_t sl = (slotw[v / SPW] >> ((v % SPW) * SBITS)) & SNONE;
+                    if (want_nh && sl != SNONE && lx != kUn && lx != 0)
+                        e[k] = W > 0 ? v * W + (int)sl : row_ptr[v] + (int)sl;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                h[k] = -1;
+                pt[k] = -1;
+                if (e[k] >= 0) {
+                    h[k] = W > 0 ? ell_col[e[k]] : col[e[k]];
+                    pt[k] = W > 0 ? ell_port[e[k]] : port[e[k]];
+                }
+            }
+            if (want_nh) {
+#pragma unroll
+                for (int k = 0; k < U; ++k) {
+                    const int v = v0 + k * (int)blockDim.x;
+                    if (v < V) {
+                        hrow[v] = h[k];
+                        prow[v] = pt[k];
+                    }
+                }
             }
         }
         __syncthreads();
@@ -647,7 +707,8 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
     // lane-packed per-destination BFS: rows of <= 32 entries, one workgroup's
     // LDS holds the levels, queue and claim bits
     const int maxrow = ctx->max_deg > ctx->max_indeg ? ctx->max_deg : ctx->max_indeg;
-    const size_t llds = bfs_lanes_words(V) * 4;
+    const int lpr = maxrow <= 4 ? 4 : maxrow <= 8 ? 8 : maxrow <= 16 ? 16 : 32;
+    const size_t llds = bfs_lanes_bytes(V, lpr);
     const bool lanes_ok = ctx->adj16 != nullptr && ctx->radj16 != nullptr && V < 65534 &&
                           maxrow <= 32 && llds <= SDNR_MAX_LDS_PER_BLOCK - 1024;
     if (lanes_ok && strcmp(force, "msbfs") != 0) {
@@ -664,20 +725,23 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
              "bfs_dest_lanes_kernel<16,sym>", "bfs_dest_lanes_kernel<32,sym>"}};
         const int li = maxrow <= 4 ? 0 : maxrow <= 8 ? 1 : maxrow <= 16 ? 2 : 3;
         ctx->last_kernel = names[sym ? 1 : 0][li];
-        // SDNROUTE_SP_LANES_G=2|4|8: frontier groups in flight per wave (tuning)
+        // SDNROUTE_SP_LANES_G=1|2|4|8: frontier groups in flight per wave
+        // (tuning; torus 32^3: 1 24.6 ms, 2 22.5 ms, 4 24.4 ms, 8 29.6 ms)
         const char *gf = getenv("SDNROUTE_SP_LANES_G");
-        const int gsel = gf ? atoi(gf) : 8;
+        const int gsel = gf ? atoi(gf) : 2;
 #define SDNR_BFS_LANES_G(LPR_, S_, G_)                                                       \
     do {                                                                                     \
         auto k = bfs_dest_lanes_kernel<LPR_, 16, G_, S_>;                                    \
         sdnr_allow_lds(reinterpret_cast<const void *>(k), llds);                             \
         hipLaunchKernelGGL(k, dim3(grid), dim3(16 * 64), llds, ctx->stream, V, ctx->W,       \
-                           ctx->adj16, ctx->radj16, ctx->row_ptr, ctx->port, ctx->ell_port,  \
-                           d_dst, ndst, d_dist, d_nh, d_nh_port);                            \
+                           ctx->adj16, ctx->radj16, ctx->row_ptr, ctx->col, ctx->port,       \
+                           ctx->ell_col, ctx->ell_port, d_dst, ndst, d_dist, d_nh,           \
+                           d_nh_port);                                                       \
     } while (0)
 #define SDNR_BFS_LANES(LPR_, S_)                                                             \
     do {                                                                                     \
-        if (gsel == 2) SDNR_BFS_LANES_G(LPR_, S_, 2);                                        \
+        if (gsel == 1) SDNR_BFS_LANES_G(LPR_, S_, 1);                                        \
+        else if (gsel == 2) SDNR_BFS_LANES_G(LPR_, S_, 2);                                   \
         else if (gsel == 4) SDNR_BFS_LANES_G(LPR_, S_, 4);                                   \
         else SDNR_BFS_LANES_G(LPR_, S_, 8);                                                  \
     } while (0)
