@@ -66,6 +66,15 @@ def parse():
     return ap.parse_args()
 
 
+def _traffic(key):
+    """PMC-measured HBM bytes per launch recorded by tools/summarize_profile.py
+    (profiles/traffic.json), or None."""
+    try:
+        return json.load(open(TRAFFIC_FILE)).get(key)
+    except Exception:   # noqa: BLE001 -- missing / unreadable file: unmeasured
+        return None
+
+
 def algorithmic_bytes_per_source(V, E, mode, packed=False):
     if mode == "dfs":
         # row_ptr + col (CSR read per source) + tree-edge port reads + table writes
@@ -291,7 +300,8 @@ def main_ecmp(args, world, rank, local, dev):
             "max_routes_per_pair": int(paths.max().item()),
             "parallelism": "destinations sharded over %d GPU(s)" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": _traffic("%s/ecmp/N%d" % (
+                         args.fabric, world)),
                      "kernel": ctx.last_kernel(), "kernel_ms": kern_ms,
                      "bytes_per_launch": bytes_launch},
     }
