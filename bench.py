@@ -125,6 +125,44 @@ def cpu_baseline(fabric, csr, srcs, hosts_per_src, H, budget_s):
     return out, ref
 
 
+_MP_DB = None
+
+
+def _mp_pairs(args):
+    """Worker of the multi-process per-pair baseline: random pairs for
+    `secs` seconds over the fork-inherited _MP_DB."""
+    from oracle import oracle as O
+    seed, secs = args
+    db, macs = _MP_DB
+    rng = np.random.default_rng(seed)
+    t0 = time.perf_counter()
+    k = 0
+    while time.perf_counter() - t0 < secs:
+        a, b = rng.integers(0, len(macs), 2)
+        O.find_route_pair(db, macs[a], macs[b])
+        k += 1
+    return k, time.perf_counter() - t0
+
+
+def cpu_reference_path_mp(fabric, secs=5.0):
+    """SURVEY.md 8(d) CPU baseline (ii) on all host cores: the per-pair Python
+    restatement in one process per core (fork, BEFORE any GPU call -- the
+    children never touch the GPU), rate = sum of the per-process rates."""
+    import multiprocessing as mp
+    global _MP_DB
+    procs = max(1, min(16, os.cpu_count() or 1))
+    db = _DictDB()
+    fabric.populate(db)
+    _MP_DB = (db, fabric.host_macs())
+    with mp.get_context("fork").Pool(procs) as pool:
+        res = pool.map(_mp_pairs, [(1000 + i, secs) for i in range(procs)])
+    _MP_DB = None
+    rate = sum(k / dt for k, dt in res)
+    return {"value": rate, "unit": "routes/s", "cores": procs, "kind": "port",
+            "sample": "oracle.find_route_pair in %d forked processes, %d random host pairs "
+                      "in %.1f s each" % (procs, sum(k for k, _ in res), secs)}
+
+
 class _DictDB(object):
     def __init__(self):
         self.switches, self.links, self.hosts = {}, {}, {}
@@ -370,6 +408,11 @@ def main():
     # path on a one-GPU box); the driver never sets it
     if os.environ.get("BENCH_DEVICE"):
         local = int(os.environ["BENCH_DEVICE"])
+    ref_mp = None
+    if world == 1 and args.mode == "dfs" and not args.no_cpu_baseline:
+        # forks: must run before the first GPU call of this process
+        ref_mp = cpu_reference_path_mp(T.by_name(args.fabric),
+                                       secs=min(5.0, args.cpu_budget_s / 4))
     if world > 1:
         backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")   # gloo: rehearsal only
         if backend == "nccl":
@@ -547,6 +590,8 @@ def main():
         base, ref = cpu_baseline(fabric, csr, srcs, counts, H, args.cpu_budget_s)
         out["cpu_baseline"] = base
         out["cpu_reference_path"] = ref
+        if ref_mp is not None:
+            out["cpu_reference_path_all_cores"] = ref_mp
         out["gpu_over_cpu"] = value / base["value"]
     if rank == 0:
         print(json.dumps(out), flush=True)
