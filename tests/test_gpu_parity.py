@@ -177,9 +177,12 @@ def test_dfs_fullsize_tree_properties(ctx):
             assert k < hi and csr.col[k] == v and csr.port[k] == t[s, v]
 
 
-@pytest.mark.parametrize("strategy", ["auto", "msbfs", "lanes"])
+@pytest.mark.parametrize("strategy", ["auto", "msbfs", "lanes", "lanes-csr"])
 @pytest.mark.parametrize("name", G.SMALL)
 def test_shortest_small_all_destinations(ctx, monkeypatch, name, strategy):
+    if strategy == "lanes-csr":                  # no ELL copy: 64-wide rows + CSR ports
+        monkeypatch.setenv("SDNROUTE_ELL", "0")
+        strategy = "lanes"
     if strategy != "auto":
         monkeypatch.setenv("SDNROUTE_SP_STRATEGY", strategy)
     fabric = G.Golden(name).fabric()
