@@ -1652,8 +1652,17 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
     } while (0)
 #define SDNR_ASYNC(N_, H_) SDNR_ASYNC_P(N_, H_, false)
         if (packed) {
-            ctx->last_kernel = "dfs_async_kernel<4,packed>";
-            SDNR_ASYNC_P(4, false, true);
+            static const char *pnames[] = {"", "", "dfs_async_kernel<2,packed>",
+                                           "dfs_async_kernel<3,packed>",
+                                           "dfs_async_kernel<4,packed>",
+                                           "dfs_async_kernel<5,packed>",
+                                           "dfs_async_kernel<6,packed>"};
+            ctx->last_kernel = pnames[nw];
+            if (nw == 2) SDNR_ASYNC_P(2, false, true);
+            else if (nw == 3) SDNR_ASYNC_P(3, false, true);
+            else if (nw == 5) SDNR_ASYNC_P(5, false, true);
+            else if (nw == 6) SDNR_ASYNC_P(6, false, true);
+            else SDNR_ASYNC_P(4, false, true);
         } else if (nw == 2) {
             if (hops) SDNR_ASYNC(2, true); else SDNR_ASYNC(2, false);
         } else if (nw == 3) {

@@ -108,6 +108,20 @@ def test_dfs_packed_fullsize_k48(ctx):
     np.testing.assert_array_equal(tree, _pack(po, to))
 
 
+@pytest.mark.parametrize("waves", [2, 3, 5, 6])
+@pytest.mark.parametrize("name", ["fat_tree_k8", "jellyfish_n60_r5", "torus_5x3x2"])
+def test_dfs_packed_async_waves(ctx, monkeypatch, name, waves):
+    _strategy(monkeypatch, "async")
+    monkeypatch.setenv("SDNROUTE_DFS_ASYNC_WAVES", str(waves))
+    csr = G.Golden(name).fabric().csr()
+    srcs = np.arange(csr.V, dtype=np.int32)
+    ctx.upload(csr)
+    tree = ctx.dfs_tables_packed(srcs)
+    assert ctx.last_kernel() == f"dfs_async_kernel<{waves},packed>"
+    po, to, _ = O.dfs_tables(csr, srcs, with_hops=False, nthreads=NTHREADS)
+    np.testing.assert_array_equal(tree, _pack(po, to))
+
+
 def test_dfs_packed_rejects_wide_ports(ctx):
     from sdnmpi_amd.topologies import CSR
     c = CSR(np.array([1, 2]), np.array([0, 1, 2]), np.array([1, 0]), np.array([0xFFFF, 3]))
