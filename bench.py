@@ -241,6 +241,7 @@ def main_flows(args, world, rank, local, dev):
         step(timing=True)
         kms.append(ctx.last_kernel_ms())        # waits for this step's walk kernel
     torch.cuda.synchronize(dev)
+    ctx.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -315,6 +316,7 @@ def main_ecmp(args, world, rank, local, dev):
         ctx.ecmp_counts_device(dist_t.data_ptr(), per, paths.data_ptr(), timing=True)
         kms.append(ctx.last_kernel_ms())
     torch.cuda.synchronize(dev)
+    ctx.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -375,11 +377,12 @@ def main_apsp(args, world, rank, local, dev):
         ctx.apsp_device(d.data_ptr(), timing=True)
         kms.append(ctx.last_kernel_ms())
     torch.cuda.synchronize(dev)
+    ctx.synchronize()
     ms = (time.perf_counter() - t0) / args.steps * 1e3
     kern_ms = float(np.mean(kms))
-    nb = (V + 63) // 64
-    Vp = nb * 64
-    ops = 2.0 * Vp ** 3                     # one add + one min per (i, j, k)
+    passes = ctx.last_launches()            # squaring passes of one APSP call
+    Vp = (V + 127) // 128 * 128             # 128x128 output tiles (apsp.hip MT)
+    ops = passes * 2.0 * Vp ** 3            # one add + one min per (i, j, k) per pass
     achieved = ops / (kern_ms / 1e3) / 1e12
     # VALU peak: 256 CUs x 4 SIMDs x 32 lanes x 2 (packed u16) ops/clk x 2.4 GHz
     peak = 256 * 4 * 32 * 2 * 2.4e9 / 1e12
@@ -392,7 +395,7 @@ def main_apsp(args, world, rank, local, dev):
         "config": {"workload": "%s APSP (V=%d)" % (args.fabric, V), "fabric": args.fabric, "V": V},
         "roofline": {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "Tops/s",
                      "frac": achieved / peak, "traffic": None, "kernel": ctx.last_kernel(),
-                     "kernel_ms": kern_ms, "ops_per_launch": ops},
+                     "kernel_ms": kern_ms, "ops_per_launch": ops, "passes": passes},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -510,6 +513,7 @@ def main():
         step(evs[i])
     drain()
     torch.cuda.synchronize(dev)
+    ctx.synchronize()          # raises if a kernel's bounded wait tripped: tables invalid
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0

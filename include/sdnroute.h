@@ -65,6 +65,23 @@ int sdnr_device_count(int *count);
 int sdnr_create(int device, sdnr_ctx **out);
 int sdnr_destroy(sdnr_ctx *ctx);
 
+/* A context over several devices of one node (the controller's single
+ * TopologyDB, reference sdnmpi/topology.py:67, driving all of them; SURVEY.md
+ * 8(e)).  devices[0] is the primary: device-pointer buffers live there and
+ * asynchronous work is ordered on its stream.  Every device holds a copy of
+ * the uploaded graph; sdnr_dfs_tables, sdnr_dfs_tables_packed and
+ * sdnr_shortest_tables split their ids into ndev contiguous shards, one per
+ * device (each with its own stream), and assemble the rows in the caller's
+ * tables -- host buffers by one device-to-host copy per shard, primary-device
+ * buffers by peer copies over xGMI (fork/join events on the primary stream).
+ * The other entry points run on the primary device.  A device may be listed
+ * more than once (several shards on one device).  Destroy with sdnr_destroy. */
+int sdnr_create_multi(const int *devices, int ndev, sdnr_ctx **out);
+
+/* Devices of a context in shard order: *n = their number; the first
+ * min(*n, cap) are written to devices (may be NULL). */
+int sdnr_device_list(const sdnr_ctx *ctx, int *devices, int cap, int *n);
+
 /* Run subsequent asynchronous work on `hip_stream` (a hipStream_t of the
  * context's device, e.g. torch.cuda.current_stream().cuda_stream); NULL
  * restores the context's own stream. */
@@ -176,6 +193,11 @@ int sdnr_route_expand(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port,
 /* Device time in milliseconds of the main kernel(s) of the last table call
  * made with SDNR_TIMING (waits for that call to finish). */
 int sdnr_last_kernel_ms(sdnr_ctx *ctx, float *ms);
+
+/* Number of launches of the main kernel in the last table call: the
+ * min-plus squaring passes of sdnr_apsp, the BFS levels of the level-by-level
+ * shortest kernel, 1 for single-launch kernels (0 before the first call). */
+int sdnr_last_launches(const sdnr_ctx *ctx, int32_t *launches);
 
 /* Name of the kernel variant the last table call launched on this context
  * (e.g. "dfs_count_kernel<4>"; "" before the first call). */

@@ -283,7 +283,9 @@ static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp)
     // every distance <= 2^s) the largest finite distance M is < 2^s: no pair
     // is at distance M + 1 <= 2^s, so none is farther
     const int nt = Vp / MT;
+    ctx->last_launches = 0;
     for (int it = 1; it <= 40; ++it) {         // 2^40 >> any hop distance
+        ctx->last_launches = it;
         SDNR_HIP(hipMemsetAsync(changed, 0, 2 * sizeof(int), ctx->stream));
         hipLaunchKernelGGL(minplus_square_kernel, dim3(nt, nt), dim3(256), 0, ctx->stream, Vp, D,
                            changed);
@@ -325,6 +327,7 @@ int sdnr_launch_apsp(sdnr_ctx *ctx, uint16_t *d_dist)
         return SDNR_OK;
     }
     ctx->last_kernel = "apsp_phase{1,2,3}_kernel";
+    ctx->last_launches = nb;
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
     hipLaunchKernelGGL(apsp_init_kernel, dim3(1024), dim3(256), 0, ctx->stream, V, Vp,
                        ctx->row_ptr, ctx->col, D);

@@ -138,6 +138,8 @@ int sdnr_create(int device, sdnr_ctx **out)
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&c->d_err), sizeof(int));
     if (e == hipSuccess) e = hipMemset(c->d_err, 0, sizeof(int));
     if (e != hipSuccess) {
@@ -149,9 +151,55 @@ int sdnr_create(int device, sdnr_ctx **out)
     return SDNR_OK;
 }
 
+int sdnr_create_multi(const int *devices, int ndev, sdnr_ctx **out)
+{
+    if (!out) return sdnr_fail(SDNR_ERR_INVAL, "sdnr_create_multi: null out");
+    *out = nullptr;
+    if (!devices || ndev < 1)
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_create_multi: %d devices", ndev);
+    sdnr_ctx *c = nullptr;
+    int rc = sdnr_create(devices[0], &c);
+    if (rc) return rc;
+    if (ndev > 1) {
+        c->peers = new sdnr_ctx *[ndev - 1]();
+        for (int k = 1; k < ndev; ++k) {
+            if ((rc = sdnr_create(devices[k], &c->peers[k - 1]))) {
+                const int keep = rc;
+                char msg[512];
+                snprintf(msg, sizeof msg, "%s", g_err);
+                sdnr_destroy(c);
+                return sdnr_fail(keep, "sdnr_create_multi: device %d: %s", devices[k], msg);
+            }
+            c->npeers = k;
+        }
+        // direct xGMI access between the primary and every other device: the
+        // peers read their shard of the ids from, and copy their tables into,
+        // the primary device's buffers
+        for (int k = 1; k < ndev; ++k) {
+            const int a = devices[0], b = devices[k];
+            if (a == b) continue;
+            int can = 0;
+            for (int dir = 0; dir < 2; ++dir) {
+                const int x = dir ? b : a, y = dir ? a : b;
+                if (hipDeviceCanAccessPeer(&can, x, y) == hipSuccess && can &&
+                    hipSetDevice(x) == hipSuccess &&
+                    hipDeviceEnablePeerAccess(y, 0) != hipSuccess)
+                    (void)hipGetLastError();     // already enabled: fine
+            }
+        }
+        (void)hipSetDevice(devices[0]);
+    }
+    *out = c;
+    return SDNR_OK;
+}
+
 int sdnr_destroy(sdnr_ctx *ctx)
 {
     if (!ctx) return SDNR_OK;
+    for (int k = 0; k < ctx->npeers; ++k) sdnr_destroy(ctx->peers[k]);
+    delete[] ctx->peers;
+    ctx->peers = nullptr;
+    ctx->npeers = 0;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     free_graph(ctx);
@@ -161,6 +209,8 @@ int sdnr_destroy(sdnr_ctx *ctx)
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
     return SDNR_OK;
@@ -176,15 +226,46 @@ int sdnr_set_stream(sdnr_ctx *ctx, void *hip_stream)
 int sdnr_synchronize(sdnr_ctx *ctx)
 {
     CHECK_CTX(ctx);
+    int first = SDNR_OK;
+    for (int k = 0; k < ctx->npeers; ++k) {
+        const int rc = sdnr_synchronize(ctx->peers[k]);
+        if (rc && !first) first = rc;
+    }
     SDNR_HIP(hipSetDevice(ctx->device));
     SDNR_HIP(hipStreamSynchronize(ctx->stream));
-    return sdnr_check_watchdog(ctx);
+    const int rc = sdnr_check_watchdog(ctx);
+    return first ? first : rc;
 }
+
+int sdnr_device_list(const sdnr_ctx *ctx, int *devices, int cap, int *n)
+{
+    CHECK_CTX(ctx);
+    if (!n) return sdnr_fail(SDNR_ERR_INVAL, "sdnr_device_list: null n");
+    *n = 1 + ctx->npeers;
+    for (int k = 0; k < *n && k < cap && devices; ++k)
+        devices[k] = k == 0 ? ctx->device : ctx->peers[k - 1]->device;
+    return SDNR_OK;
+}
+
+static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_ptr,
+                            const int32_t *col, const int32_t *port);
 
 int sdnr_graph_upload(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_ptr,
                       const int32_t *col, const int32_t *port)
 {
     CHECK_CTX(ctx);
+    int rc = graph_upload_one(ctx, V, E, row_ptr, col, port);
+    // every shard's device holds the whole graph (replicated CSR)
+    for (int k = 0; k < ctx->npeers && !rc; ++k)
+        rc = graph_upload_one(ctx->peers[k], V, E, row_ptr, col, port);
+    if (rc) return rc;
+    SDNR_HIP(hipSetDevice(ctx->device));
+    return SDNR_OK;
+}
+
+static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_ptr,
+                            const int32_t *col, const int32_t *port)
+{
     if (V < 0 || E < 0) return sdnr_fail(SDNR_ERR_INVAL, "graph_upload: V=%d E=%d", V, E);
     if (!row_ptr || (E > 0 && (!col || !port)))
         return sdnr_fail(SDNR_ERR_INVAL, "graph_upload: null array");
@@ -360,7 +441,133 @@ static int begin_call(sdnr_ctx *ctx, int32_t n, const void *ids, uint32_t flags,
     }
     SDNR_HIP(hipSetDevice(ctx->device));
     ctx->timed = (flags & SDNR_TIMING) != 0;
+    ctx->last_launches = 1;
     return SDNR_OK;
+}
+
+// One table call over the context and its peers (sdnr_create_multi): the ids
+// are split into contiguous shards, shard k runs on context k, and up to three
+// [n][V] output tables (entry sizes es[i], null outputs skipped) are assembled
+// in the caller's buffers.
+//  * host buffers: every context stages its shard, launches, and copies its
+//    rows straight into the caller's tables; then all are waited for and
+//    their watchdog words checked.
+//  * device buffers (on the primary device, asynchronous on its stream): the
+//    peers wait for the primary stream (fork event), pull their ids over
+//    xGMI, compute into their own scratch and copy the rows into the primary
+//    device's tables; the primary stream waits for every peer (join events).
+typedef int (*shard_launch_fn)(sdnr_ctx *c, const int32_t *ids, int32_t n, void *const out[3]);
+
+static int run_sharded(sdnr_ctx *ctx, const int32_t *ids, int32_t n, void *const out[3],
+                       const size_t es[3], uint32_t flags, shard_launch_fn launch)
+{
+    const int nctx = 1 + ctx->npeers;
+    const size_t V = (size_t)ctx->V;
+    const int32_t per = (n + nctx - 1) / nctx;
+    auto sub = [&](int k) { return k == 0 ? ctx : ctx->peers[k - 1]; };
+    auto lo_of = [&](int k) { return (int32_t)((int64_t)k * per < n ? (int64_t)k * per : n); };
+    auto hi_of = [&](int k) { return lo_of(k) + per < n ? lo_of(k) + per : n; };
+    const bool timed = ctx->timed;
+    int rc;
+    if (flags & SDNR_DEVICE_PTRS) {
+        if (nctx == 1) return launch(ctx, ids, n, out);
+        if (timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
+        SDNR_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
+        for (int k = 1; k < nctx; ++k) {           // peers first: they run meanwhile
+            sdnr_ctx *c = sub(k);
+            const int32_t lo = lo_of(k), cnt = hi_of(k) - lo;
+            if (cnt <= 0) continue;
+            SDNR_HIP(hipSetDevice(c->device));
+            SDNR_HIP(hipStreamWaitEvent(c->stream, ctx->ev_fork, 0));
+            size_t need = 4 * (size_t)cnt + 256;
+            for (int i = 0; i < 3; ++i)
+                if (out[i]) need += (size_t)cnt * V * es[i] + 256;
+            if ((rc = sdnr_reserve(&c->stage, &c->stage_bytes, need))) return rc;
+            Stage st{static_cast<char *>(c->stage)};
+            int32_t *d_ids = static_cast<int32_t *>(st.take(4 * (size_t)cnt));
+            void *d_out[3] = {nullptr, nullptr, nullptr};
+            for (int i = 0; i < 3; ++i)
+                if (out[i]) d_out[i] = st.take((size_t)cnt * V * es[i]);
+            SDNR_HIP(hipMemcpyPeerAsync(d_ids, c->device, ids + lo, ctx->device, 4 * (size_t)cnt,
+                                        c->stream));
+            c->timed = false;
+            if ((rc = launch(c, d_ids, cnt, d_out))) return rc;
+            for (int i = 0; i < 3; ++i)
+                if (out[i])
+                    SDNR_HIP(hipMemcpyPeerAsync(static_cast<char *>(out[i]) + (size_t)lo * V * es[i],
+                                                ctx->device, d_out[i], c->device,
+                                                (size_t)cnt * V * es[i], c->stream));
+            SDNR_HIP(hipEventRecord(c->ev_join, c->stream));
+        }
+        SDNR_HIP(hipSetDevice(ctx->device));
+        ctx->timed = false;                        // the span is timed around fork/join
+        rc = launch(ctx, ids, hi_of(0), out);
+        ctx->timed = timed;
+        if (rc) return rc;
+        for (int k = 1; k < nctx; ++k)
+            if (hi_of(k) > lo_of(k)) SDNR_HIP(hipStreamWaitEvent(ctx->stream, sub(k)->ev_join, 0));
+        if (timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+        return SDNR_OK;
+    }
+    // host buffers: stage + launch everywhere, then copy out, then wait
+    void *d_outs[64][3] = {};
+    if (nctx > 64) return sdnr_fail(SDNR_ERR_INVAL, "more than 64 devices");
+    for (int k = 0; k < nctx; ++k) {
+        sdnr_ctx *c = sub(k);
+        const int32_t lo = lo_of(k), cnt = hi_of(k) - lo;
+        if (cnt <= 0) continue;
+        SDNR_HIP(hipSetDevice(c->device));
+        size_t need = 4 * (size_t)cnt + 256;
+        for (int i = 0; i < 3; ++i)
+            if (out[i]) need += (size_t)cnt * V * es[i] + 256;
+        if ((rc = sdnr_reserve(&c->stage, &c->stage_bytes, need))) return rc;
+        Stage st{static_cast<char *>(c->stage)};
+        int32_t *d_ids = static_cast<int32_t *>(st.take(4 * (size_t)cnt));
+        for (int i = 0; i < 3; ++i)
+            if (out[i]) d_outs[k][i] = st.take((size_t)cnt * V * es[i]);
+        SDNR_HIP(hipMemcpyAsync(d_ids, ids + lo, 4 * (size_t)cnt, hipMemcpyHostToDevice, c->stream));
+        c->timed = k == 0 && nctx == 1 && timed;  // multi: shard 0 alone is not the span
+        if ((rc = launch(c, d_ids, cnt, d_outs[k]))) return rc;
+    }
+    for (int k = 0; k < nctx; ++k) {
+        sdnr_ctx *c = sub(k);
+        const int32_t lo = lo_of(k), cnt = hi_of(k) - lo;
+        if (cnt <= 0) continue;
+        SDNR_HIP(hipSetDevice(c->device));
+        for (int i = 0; i < 3; ++i)
+            if (out[i])
+                SDNR_HIP(hipMemcpyAsync(static_cast<char *>(out[i]) + (size_t)lo * V * es[i],
+                                        d_outs[k][i], (size_t)cnt * V * es[i],
+                                        hipMemcpyDeviceToHost, c->stream));
+    }
+    int first = SDNR_OK;
+    for (int k = 0; k < nctx; ++k) {
+        sdnr_ctx *c = sub(k);
+        SDNR_HIP(hipSetDevice(c->device));
+        SDNR_HIP(hipStreamSynchronize(c->stream));
+        rc = sdnr_check_watchdog(c);
+        if (rc && !first) first = rc;
+    }
+    ctx->timed = timed;
+    SDNR_HIP(hipSetDevice(ctx->device));
+    return first;
+}
+
+static int shard_dfs(sdnr_ctx *c, const int32_t *ids, int32_t n, void *const o[3])
+{
+    return sdnr_launch_dfs(c, ids, n, static_cast<int32_t *>(o[0]), static_cast<int32_t *>(o[1]),
+                           static_cast<int32_t *>(o[2]), nullptr);
+}
+
+static int shard_dfs_packed(sdnr_ctx *c, const int32_t *ids, int32_t n, void *const o[3])
+{
+    return sdnr_launch_dfs(c, ids, n, nullptr, nullptr, nullptr, static_cast<uint32_t *>(o[0]));
+}
+
+static int shard_shortest(sdnr_ctx *c, const int32_t *ids, int32_t n, void *const o[3])
+{
+    return sdnr_launch_shortest(c, ids, n, static_cast<uint16_t *>(o[0]),
+                                static_cast<int32_t *>(o[1]), static_cast<int32_t *>(o[2]));
 }
 
 int sdnr_dfs_tables(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc, int32_t *parent,
@@ -370,22 +577,9 @@ int sdnr_dfs_tables(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc, int32_t *pa
     if (rc) return rc;
     if (nsrc > 0 && (!parent || !port))
         return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_tables: null table");
-    if (flags & SDNR_DEVICE_PTRS) return sdnr_launch_dfs(ctx, src, nsrc, parent, port, hops, nullptr);
-    const size_t V = (size_t)ctx->V, rows = (size_t)nsrc * V;
-    const size_t need = 4 * (size_t)nsrc + 256 + (rows * 4 + 256) * (hops ? 3 : 2);
-    if ((rc = sdnr_reserve(&ctx->stage, &ctx->stage_bytes, need))) return rc;
-    Stage st{static_cast<char *>(ctx->stage)};
-    int32_t *d_src = static_cast<int32_t *>(st.take(4 * (size_t)nsrc));
-    int32_t *d_par = static_cast<int32_t *>(st.take(rows * 4));
-    int32_t *d_prt = static_cast<int32_t *>(st.take(rows * 4));
-    int32_t *d_hop = hops ? static_cast<int32_t *>(st.take(rows * 4)) : nullptr;
-    SDNR_HIP(hipMemcpyAsync(d_src, src, 4 * (size_t)nsrc, hipMemcpyHostToDevice, ctx->stream));
-    if ((rc = sdnr_launch_dfs(ctx, d_src, nsrc, d_par, d_prt, d_hop, nullptr))) return rc;
-    SDNR_HIP(hipMemcpyAsync(parent, d_par, rows * 4, hipMemcpyDeviceToHost, ctx->stream));
-    SDNR_HIP(hipMemcpyAsync(port, d_prt, rows * 4, hipMemcpyDeviceToHost, ctx->stream));
-    if (hops) SDNR_HIP(hipMemcpyAsync(hops, d_hop, rows * 4, hipMemcpyDeviceToHost, ctx->stream));
-    SDNR_HIP(hipStreamSynchronize(ctx->stream));
-    return sdnr_check_watchdog(ctx);
+    void *const out[3] = {parent, port, hops};
+    const size_t es[3] = {4, 4, 4};
+    return run_sharded(ctx, src, nsrc, out, es, flags, shard_dfs);
 }
 
 int sdnr_dfs_tables_packed(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc, uint32_t *tree,
@@ -398,18 +592,9 @@ int sdnr_dfs_tables_packed(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc, uint
         return sdnr_fail(SDNR_ERR_INVAL,
                          "sdnr_dfs_tables_packed: needs V <= 65535 and ports < 0xFFFF (V=%d)",
                          ctx->V);
-    if (flags & SDNR_DEVICE_PTRS) return sdnr_launch_dfs(ctx, src, nsrc, nullptr, nullptr, nullptr, tree);
-    const size_t V = (size_t)ctx->V, rows = (size_t)nsrc * V;
-    if ((rc = sdnr_reserve(&ctx->stage, &ctx->stage_bytes, 4 * (size_t)nsrc + 256 + rows * 4)))
-        return rc;
-    Stage st{static_cast<char *>(ctx->stage)};
-    int32_t *d_src = static_cast<int32_t *>(st.take(4 * (size_t)nsrc));
-    uint32_t *d_tree = static_cast<uint32_t *>(st.take(rows * 4));
-    SDNR_HIP(hipMemcpyAsync(d_src, src, 4 * (size_t)nsrc, hipMemcpyHostToDevice, ctx->stream));
-    if ((rc = sdnr_launch_dfs(ctx, d_src, nsrc, nullptr, nullptr, nullptr, d_tree))) return rc;
-    SDNR_HIP(hipMemcpyAsync(tree, d_tree, rows * 4, hipMemcpyDeviceToHost, ctx->stream));
-    SDNR_HIP(hipStreamSynchronize(ctx->stream));
-    return sdnr_check_watchdog(ctx);
+    void *const out[3] = {tree, nullptr, nullptr};
+    const size_t es[3] = {4, 0, 0};
+    return run_sharded(ctx, src, nsrc, out, es, flags, shard_dfs_packed);
 }
 
 int sdnr_shortest_tables(sdnr_ctx *ctx, const int32_t *dst, int32_t ndst, uint16_t *dist,
@@ -420,24 +605,9 @@ int sdnr_shortest_tables(sdnr_ctx *ctx, const int32_t *dst, int32_t ndst, uint16
     if (ndst > 0 && !dist) return sdnr_fail(SDNR_ERR_INVAL, "sdnr_shortest_tables: null dist");
     if ((nh == nullptr) != (nh_port == nullptr))
         return sdnr_fail(SDNR_ERR_INVAL, "sdnr_shortest_tables: nh and nh_port go together");
-    if (flags & SDNR_DEVICE_PTRS) return sdnr_launch_shortest(ctx, dst, ndst, dist, nh, nh_port);
-    const size_t V = (size_t)ctx->V, rows = (size_t)ndst * V;
-    const size_t need = 4 * (size_t)ndst + 256 + rows * 2 + 256 + (nh ? 2 * (rows * 4 + 256) : 0);
-    if ((rc = sdnr_reserve(&ctx->stage, &ctx->stage_bytes, need))) return rc;
-    Stage st{static_cast<char *>(ctx->stage)};
-    int32_t *d_dst = static_cast<int32_t *>(st.take(4 * (size_t)ndst));
-    uint16_t *d_dist = static_cast<uint16_t *>(st.take(rows * 2));
-    int32_t *d_nh = nh ? static_cast<int32_t *>(st.take(rows * 4)) : nullptr;
-    int32_t *d_np = nh ? static_cast<int32_t *>(st.take(rows * 4)) : nullptr;
-    SDNR_HIP(hipMemcpyAsync(d_dst, dst, 4 * (size_t)ndst, hipMemcpyHostToDevice, ctx->stream));
-    if ((rc = sdnr_launch_shortest(ctx, d_dst, ndst, d_dist, d_nh, d_np))) return rc;
-    SDNR_HIP(hipMemcpyAsync(dist, d_dist, rows * 2, hipMemcpyDeviceToHost, ctx->stream));
-    if (nh) {
-        SDNR_HIP(hipMemcpyAsync(nh, d_nh, rows * 4, hipMemcpyDeviceToHost, ctx->stream));
-        SDNR_HIP(hipMemcpyAsync(nh_port, d_np, rows * 4, hipMemcpyDeviceToHost, ctx->stream));
-    }
-    SDNR_HIP(hipStreamSynchronize(ctx->stream));
-    return SDNR_OK;
+    void *const out[3] = {dist, nh, nh_port};
+    const size_t es[3] = {2, 4, 4};
+    return run_sharded(ctx, dst, ndst, out, es, flags, shard_shortest);
 }
 
 int sdnr_apsp(sdnr_ctx *ctx, uint16_t *dist, uint32_t flags)
@@ -604,6 +774,14 @@ int sdnr_ecmp_routes(sdnr_ctx *ctx, const uint16_t *dist, const uint64_t *paths,
 }
 
 const char *sdnr_last_kernel(const sdnr_ctx *ctx) { return ctx ? ctx->last_kernel : ""; }
+
+int sdnr_last_launches(const sdnr_ctx *ctx, int32_t *launches)
+{
+    CHECK_CTX(ctx);
+    if (!launches) return sdnr_fail(SDNR_ERR_INVAL, "sdnr_last_launches: null out");
+    *launches = ctx->last_launches;
+    return SDNR_OK;
+}
 
 int sdnr_last_kernel_ms(sdnr_ctx *ctx, float *ms)
 {

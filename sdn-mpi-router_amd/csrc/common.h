@@ -72,7 +72,17 @@ struct sdnr_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     const char *last_kernel = "";       // variant launched by the last table call
+    int32_t last_launches = 0;          // main-kernel launches of the last table call
     int *d_err = nullptr;               // kernel watchdog word (0 = ok)
+
+    // multi-device context (sdnr_create_multi): this context is shard 0 on
+    // the primary device; peers[k] own shard k+1 (own device, stream, graph
+    // copy and scratch).  fork/join events order the peers' streams after /
+    // before the primary stream.
+    sdnr_ctx **peers = nullptr;
+    int npeers = 0;
+    hipEvent_t ev_fork = nullptr;       // recorded on the primary stream
+    hipEvent_t ev_join = nullptr;       // per context: recorded on its own stream
 };
 
 // Raise a kernel's dynamic-LDS limit; a refusal (e.g. static LDS + bytes >

@@ -17,6 +17,9 @@
 //    into the one whose count range holds r (r -= paths[n] for the ones
 //    skipped).  One thread per route; the vertex sequence is written to a
 //    fixed-stride slot.
+#include <stdlib.h>
+#include <string.h>
+
 #include "common.h"
 
 namespace {
@@ -173,6 +176,47 @@ __global__ __launch_bounds__(NW * 64) void ecmp_count_rows_kernel(
     }
 }
 
+// Graphs whose row state does not fit one workgroup's LDS (torus 32^3,
+// Jellyfish 100k): the same level DP with the counts kept in the output row
+// itself (global memory) and the levels read from the dist row.  Level L's
+// vertices are found by a sweep of the dist row; each one sums its CSR
+// out-neighbours one level closer.  Only this workgroup touches the row, so
+// a barrier (workgroup-scope release/acquire, same CU) orders the levels.
+__global__ __launch_bounds__(1024) void ecmp_count_global_kernel(
+    int V, int ndst, const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+    const uint16_t *__restrict__ dist, uint64_t *__restrict__ paths)
+{
+    __shared__ int maxd;
+    for (int row = blockIdx.x; row < ndst; row += gridDim.x) {
+        const uint16_t *drow = dist + (size_t)row * V;
+        uint64_t *prow = paths + (size_t)row * V;
+        if (threadIdx.x == 0) maxd = 0;
+        __syncthreads();
+        int mymax = 0;
+        for (int x = threadIdx.x; x < V; x += blockDim.x) {
+            const uint16_t dx = drow[x];
+            prow[x] = dx == 0 ? 1ull : 0ull;
+            if (dx != 0xFFFFu && dx > mymax) mymax = dx;
+        }
+        atomicMax(&maxd, mymax);
+        __syncthreads();
+        const int top = maxd;
+        for (int L = 1; L <= top; ++L) {
+            for (int x = threadIdx.x; x < V; x += blockDim.x) {
+                if (drow[x] != (uint16_t)L) continue;
+                uint64_t c = 0;
+                const int re = row_ptr[x + 1];
+                for (int e = row_ptr[x]; e < re; ++e) {
+                    const int n = col[e];
+                    if (drow[n] == (uint16_t)(L - 1)) c = sat_add(c, prow[n]);
+                }
+                prow[x] = c;
+            }
+            __syncthreads();
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void ecmp_unrank_kernel(
     int V, const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
     const uint16_t *__restrict__ dist, const uint64_t *__restrict__ paths,
@@ -223,8 +267,11 @@ int sdnr_launch_ecmp_counts(sdnr_ctx *ctx, const uint16_t *d_dist, int32_t ndst,
     // thread-per-vertex kernel over the 64-wide rows when they exist
     constexpr int NW = 4;
     const size_t cap = SDNR_MAX_LDS_PER_BLOCK - 1024;
-    const bool rows_ok = ctx->adj16 != nullptr && ctx->deg32 != nullptr && V < 65534 &&
-                         ecmp_wave_lds(V, NW, false) <= cap;
+    // SDNROUTE_ECMP=global forces the global-memory DP (tests)
+    const char *ef = getenv("SDNROUTE_ECMP");
+    const bool force_global = ef && !strcmp(ef, "global");
+    const bool rows_ok = !force_global && ctx->adj16 != nullptr && ctx->deg32 != nullptr &&
+                         V < 65534 && ecmp_wave_lds(V, NW, false) <= cap;
     if (rows_ok) {
         const bool stage = ecmp_wave_lds(V, NW, true) <= cap;
         const size_t wlds = ecmp_wave_lds(V, NW, stage);
@@ -241,8 +288,18 @@ int sdnr_launch_ecmp_counts(sdnr_ctx *ctx, const uint16_t *d_dist, int32_t ndst,
         return SDNR_OK;
     }
     const size_t lds = (size_t)V * 10;
-    if (lds > SDNR_MAX_LDS_PER_BLOCK - 1024)
-        return sdnr_fail(SDNR_ERR_INVAL, "ecmp counts: V=%d too large for one workgroup", V);
+    if (force_global || lds > SDNR_MAX_LDS_PER_BLOCK - 1024) {
+        // row state in global memory (the output row); one workgroup per row
+        int grid = ctx->num_cus * 4;
+        if (grid > ndst) grid = ndst;
+        ctx->last_kernel = "ecmp_count_global_kernel";
+        if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
+        hipLaunchKernelGGL(ecmp_count_global_kernel, dim3(grid), dim3(1024), 0, ctx->stream, V,
+                           ndst, ctx->row_ptr, ctx->col, d_dist, d_paths);
+        SDNR_HIP(hipGetLastError());
+        if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+        return SDNR_OK;
+    }
     int grid = ctx->num_cus * 2;
     if (grid > ndst) grid = ndst;
     sdnr_allow_lds(reinterpret_cast<const void *>(ecmp_count_kernel), lds);

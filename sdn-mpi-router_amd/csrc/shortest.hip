@@ -784,7 +784,9 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
                            ctx->stream, V, d_dst, ndst, front, vis, d_dist);
         SDNR_HIP(hipGetLastError());
         int h_changed = 1;
+        ctx->last_launches = 0;
         for (int lvl = 1; lvl < 0xFFFF && h_changed; ++lvl) {
+            ctx->last_launches = lvl;
             SDNR_HIP(hipMemsetAsync(changed, 0, sizeof(int), ctx->stream));
             hipLaunchKernelGGL(msbfs_level_kernel, dim3((V + 255) / 256, nbatch), dim3(256),
                                0, ctx->stream, V, ctx->W, ctx->row_ptr, ctx->col, ctx->ell_col,

@@ -32,11 +32,11 @@ ABI_VERSION = 1
 # every entry point declared in include/sdnroute.h
 EXPORTED_SYMBOLS = (
     "sdnr_abi_version", "sdnr_last_error", "sdnr_device_count", "sdnr_create",
-    "sdnr_destroy", "sdnr_set_stream", "sdnr_synchronize", "sdnr_graph_upload",
+    "sdnr_create_multi", "sdnr_device_list", "sdnr_destroy", "sdnr_set_stream", "sdnr_synchronize", "sdnr_graph_upload",
     "sdnr_graph_info", "sdnr_dfs_tables", "sdnr_dfs_tables_packed", "sdnr_shortest_tables",
     "sdnr_apsp", "sdnr_route_offsets", "sdnr_route_expand", "sdnr_ecmp_counts",
     "sdnr_ecmp_routes",
-    "sdnr_last_kernel_ms", "sdnr_last_kernel",
+    "sdnr_last_kernel_ms", "sdnr_last_kernel", "sdnr_last_launches",
 )
 
 
@@ -65,6 +65,8 @@ def _bind(L):
         "sdnr_last_error": ([], ctypes.c_char_p),
         "sdnr_device_count": ([ctypes.POINTER(c_int)], c_int),
         "sdnr_create": ([c_int, ctypes.POINTER(vp)], c_int),
+        "sdnr_create_multi": ([ctypes.POINTER(c_int), c_int, ctypes.POINTER(vp)], c_int),
+        "sdnr_device_list": ([vp, ctypes.POINTER(c_int), c_int, ctypes.POINTER(c_int)], c_int),
         "sdnr_destroy": ([vp], c_int),
         "sdnr_set_stream": ([vp, vp], c_int),
         "sdnr_synchronize": ([vp], c_int),
@@ -81,6 +83,7 @@ def _bind(L):
         "sdnr_route_expand": ([vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp, u32], c_int),
         "sdnr_last_kernel_ms": ([vp, ctypes.POINTER(ctypes.c_float)], c_int),
         "sdnr_last_kernel": ([vp], ctypes.c_char_p),
+        "sdnr_last_launches": ([vp, ctypes.POINTER(i32)], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -144,16 +147,33 @@ def _ptr(a):
 
 
 class Context(object):
-    """One route-engine context on one HIP device (owns graph + scratch)."""
+    """A route-engine context (owns graph + scratch) on one HIP device, or --
+    ``device`` a sequence -- over several (sdnr_create_multi: the table calls
+    are sharded by source/destination over the devices, device-pointer
+    buffers live on the first one)."""
 
     def __init__(self, device=0):
         self._lib = library()
         h = ctypes.c_void_p()
-        _check(self._lib.sdnr_create(int(device), ctypes.byref(h)))
+        if isinstance(device, (list, tuple)):
+            devs = [int(d) for d in device]
+            arr = (ctypes.c_int * len(devs))(*devs)
+            _check(self._lib.sdnr_create_multi(arr, len(devs), ctypes.byref(h)))
+            self.devices = devs
+        else:
+            _check(self._lib.sdnr_create(int(device), ctypes.byref(h)))
+            self.devices = [int(device)]
         self._h = h
-        self.device = int(device)
+        self.device = self.devices[0]
         self.V = -1
         self.E = 0
+
+    def device_list(self):
+        n = ctypes.c_int()
+        _check(self._lib.sdnr_device_list(self._h, None, 0, ctypes.byref(n)))
+        arr = (ctypes.c_int * n.value)()
+        _check(self._lib.sdnr_device_list(self._h, arr, n.value, ctypes.byref(n)))
+        return list(arr)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -273,8 +293,16 @@ class Context(object):
                                           _ptr(out), 0))
         return out
 
-    def route_offsets_device(self, hops_ptr, rows_ptr, dsts_ptr, npairs, off_ptr):
-        _check(self._lib.sdnr_route_offsets(self._h, ctypes.c_void_p(hops_ptr), 0,
+    def ecmp_routes_device(self, dist_ptr, paths_ptr, ndst, rows_ptr, srcs_ptr, ranks_ptr,
+                           nroutes, max_len, out_ptr):
+        _check(self._lib.sdnr_ecmp_routes(self._h, ctypes.c_void_p(dist_ptr),
+                                          ctypes.c_void_p(paths_ptr), int(ndst),
+                                          ctypes.c_void_p(rows_ptr), ctypes.c_void_p(srcs_ptr),
+                                          ctypes.c_void_p(ranks_ptr), int(nroutes), int(max_len),
+                                          ctypes.c_void_p(out_ptr), DEVICE_PTRS))
+
+    def route_offsets_device(self, hops_ptr, rows_ptr, dsts_ptr, npairs, off_ptr, nrows=0):
+        _check(self._lib.sdnr_route_offsets(self._h, ctypes.c_void_p(hops_ptr), int(nrows),
                                             ctypes.c_void_p(rows_ptr), ctypes.c_void_p(dsts_ptr),
                                             int(npairs), ctypes.c_void_p(off_ptr), DEVICE_PTRS))
 
@@ -321,6 +349,11 @@ class Context(object):
 
     def last_kernel(self):
         return self._lib.sdnr_last_kernel(self._h).decode()
+
+    def last_launches(self):
+        n = ctypes.c_int32()
+        _check(self._lib.sdnr_last_launches(self._h, ctypes.byref(n)))
+        return n.value
 
     def last_kernel_ms(self):
         ms = ctypes.c_float()

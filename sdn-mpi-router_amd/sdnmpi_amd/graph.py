@@ -129,11 +129,10 @@ def export_graph(links, switches, hosts, key=None):
             sport.append(int(link.src.port_no))
     extra = list(switches.keys())
     extra.extend(h.port.dpid for h in hosts.values())
-    csr = build_csr(np.asarray(src, np.int64), np.asarray(dst, np.int64),
-                    np.asarray(sport, np.int64), extra_vertices=extra)
+    csr = build_csr(src, dst, np.asarray(sport, np.int64), extra_vertices=extra)
     return GraphExport(csr, key)
 
 
 def empty_csr():
-    return CSR(np.zeros(0, np.int64), np.zeros(1, np.int32), np.zeros(0, np.int32),
+    return CSR(np.zeros(0, np.uint64), np.zeros(1, np.int32), np.zeros(0, np.int32),
                np.zeros(0, np.int32))

@@ -79,39 +79,102 @@ def edge_diff(old, new):
     return EdgeDiff(split(rem), split(add), split(prt))
 
 
+class _NumpyNS(object):
+    """Array ops of the row tests on host (numpy) tables."""
+
+    @staticmethod
+    def zeros_bool(n):
+        return np.zeros(n, bool)
+
+    @staticmethod
+    def i64(a):
+        return np.asarray(a).astype(np.int64)
+
+    @staticmethod
+    def full_i64(n, v):
+        return np.full(n, v, np.int64)
+
+    @staticmethod
+    def nonzero(m):
+        return np.nonzero(m)[0]
+
+    @staticmethod
+    def host(a):
+        return a
+
+
+class _TorchNS(object):
+    """The same ops on device (torch) tables: the tests run where the tables
+    live, only the per-row verdict comes back to the host."""
+
+    def __init__(self, device):
+        import torch
+        self.t = torch
+        self.device = device
+
+    def zeros_bool(self, n):
+        return self.t.zeros(n, dtype=self.t.bool, device=self.device)
+
+    def i64(self, a):
+        if isinstance(a, np.ndarray):
+            return self.t.as_tensor(a.astype(np.int64), device=self.device)
+        return a.to(self.t.int64, copy=True)
+
+    def full_i64(self, n, v):
+        return self.t.full((n,), int(v), dtype=self.t.int64, device=self.device)
+
+    def nonzero(self, m):
+        return self.t.nonzero(m).flatten()
+
+    @staticmethod
+    def host(a):
+        return a.cpu().numpy()
+
+
+def _ns(a):
+    return _NumpyNS() if isinstance(a, np.ndarray) else _TorchNS(a.device)
+
+
+def _u16(xp, a):
+    """u16 distances as int64 (device tables hold them in int16)."""
+    d = xp.i64(a)
+    return d & 0xFFFF if str(a.dtype).endswith("int16") and "u" not in str(a.dtype) else d
+
+
 def _popped_before(parent, hops, rows, a, b):
     """bool[n]: in row ``rows[i]``'s tree, vertex a[i] is popped before b[i]
     (a != b, both reached) -- preorder, children in descending id order."""
+    xp = _ns(parent)
     n = rows.shape[0]
-    res = np.zeros(n, bool)
+    res = xp.zeros_bool(n)
     if n == 0:
         return res
-    x, y = a.astype(np.int64).copy(), b.astype(np.int64).copy()
-    hx, hy = hops[rows, x].astype(np.int64), hops[rows, y].astype(np.int64)
+    x, y = xp.i64(a), xp.i64(b)          # copies: climbed in place below
+    hx, hy = xp.i64(hops[rows, x]), xp.i64(hops[rows, y])
     a_deeper, b_deeper = hx > hy, hy > hx
     # lift the deeper vertex to the other's depth
     while True:
         sel = hx > hy
-        if not sel.any():
+        if not bool(sel.any()):
             break
-        x[sel] = parent[rows[sel], x[sel]]
+        x[sel] = xp.i64(parent[rows[sel], x[sel]])
         hx[sel] -= 1
     while True:
         sel = hy > hx
-        if not sel.any():
+        if not bool(sel.any()):
             break
-        y[sel] = parent[rows[sel], y[sel]]
+        y[sel] = xp.i64(parent[rows[sel], y[sel]])
         hy[sel] -= 1
     done = x == y                    # one is the other's ancestor
     res[done & b_deeper] = True      # a is b's ancestor: a pops first
     res[done & a_deeper] = False     # b is a's ancestor
     # climb together until the parents meet: x, y are then the LCA's children
-    while not done.all():
+    while not bool(done.all()):
         act = ~done
-        px = parent[rows[act], x[act]]
-        py = parent[rows[act], y[act]]
+        px = xp.i64(parent[rows[act], x[act]])
+        py = xp.i64(parent[rows[act], y[act]])
         meet = px == py
-        idx = np.nonzero(act)[0]
+        idx = xp.nonzero(act)
         hit = idx[meet]
         res[hit] = x[hit] > y[hit]   # larger child's branch pops first
         done[hit] = True
@@ -122,17 +185,19 @@ def _popped_before(parent, hops, rows, a, b):
 
 
 def dfs_rows_affected(parent, hops, srcs, diff):
-    """bool[S]: rows of the per-source default-route tables (parent, hops
-    [S, V], sources ``srcs``) that the link changes in ``diff`` alter."""
+    """bool[S] (numpy): rows of the per-source default-route tables (parent,
+    hops [S, V], sources ``srcs``; numpy or device tensors) that the link
+    changes in ``diff`` alter."""
+    xp = _ns(parent)
     S = parent.shape[0]
-    out = np.zeros(S, bool)
+    out = xp.zeros_bool(S)
     # removed or re-ported link (u, v): only when it is the tree edge into v
     for u, v in (diff.removed, diff.ported):
         for uu, vv in zip(u.tolist(), v.tolist()):
             out |= parent[:, vv] == uu
     # added link (u, v)
-    rows_all = np.arange(S, dtype=np.int64)
-    srcs = np.asarray(srcs, np.int64)
+    rows_all = xp.i64(np.arange(S, dtype=np.int64))
+    srcs = xp.i64(np.asarray(srcs, np.int64))
     for uu, vv in zip(diff.added[0].tolist(), diff.added[1].tolist()):
         if uu == vv:
             continue                                  # u is visited when popped
@@ -142,26 +207,27 @@ def dfs_rows_affected(parent, hops, srcs, diff):
         unreached_v = cand & (pv < 0)
         out |= unreached_v
         chk = cand & (pv >= 0)
-        if chk.any():
+        if bool(chk.any()):
             r = rows_all[chk]
-            before = _popped_before(parent, hops, r, pv[chk].astype(np.int64),
-                                    np.full(r.shape[0], uu, np.int64))
+            before = _popped_before(parent, hops, r, xp.i64(pv[chk]),
+                                    xp.full_i64(r.shape[0], uu))
             out[r[~before]] = True
-    return out
+    return xp.host(out)
 
 
 def sp_rows_affected(dist, nh, diff):
-    """bool[D]: rows of the per-destination shortest tables (dist u16 with
-    0xFFFF = unreachable, nh [D, V]) that the link changes alter."""
+    """bool[D] (numpy): rows of the per-destination shortest tables (dist
+    u16 with 0xFFFF = unreachable, nh [D, V]; numpy or device tensors) that
+    the link changes alter."""
+    xp = _ns(dist)
     D = dist.shape[0]
-    out = np.zeros(D, bool)
-    d32 = dist.astype(np.int64)
+    out = xp.zeros_bool(D)
     for u, v in (diff.removed, diff.ported):
         for xx, nn in zip(u.tolist(), v.tolist()):
             out |= nh[:, xx] == nn
     for xx, nn in zip(diff.added[0].tolist(), diff.added[1].tolist()):
-        dx, dn = d32[:, xx], d32[:, nn]
+        dx, dn = _u16(xp, dist[:, xx]), _u16(xp, dist[:, nn])
         ok = dn != _INF
-        nhx = nh[:, xx].astype(np.int64)
+        nhx = xp.i64(nh[:, xx])
         out |= ok & ((dn + 1 < dx) | ((dn + 1 == dx) & ((nhx < 0) | (nn < nhx))))
-    return out
+    return xp.host(out)

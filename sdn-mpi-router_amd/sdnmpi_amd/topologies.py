@@ -72,12 +72,15 @@ class CSR(object):
     ``dpids[i]`` is the dpid of dense vertex ``i`` (ascending, so row order of
     ``col`` equals ``sorted(links[u].keys())``); ``col``/``port`` give the
     destination vertex and ``links[u][v].src.port_no`` of every directed link.
+    Datapath ids are unsigned 64-bit in OpenFlow (ofp_switch_features.
+    datapath_id), so ``dpids`` is uint64 and the whole range sorts as the
+    reference's Python ints do.
     """
 
     __slots__ = ("dpids", "row_ptr", "col", "port")
 
     def __init__(self, dpids, row_ptr, col, port):
-        self.dpids = np.ascontiguousarray(dpids, dtype=np.int64)
+        self.dpids = np.ascontiguousarray(dpids, dtype=np.uint64)
         self.row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int32)
         self.col = np.ascontiguousarray(col, dtype=np.int32)
         self.port = np.ascontiguousarray(port, dtype=np.int32)
@@ -91,7 +94,7 @@ class CSR(object):
         return int(self.col.shape[0])
 
     def index_of(self, dpids):
-        d = np.asarray(dpids, dtype=np.int64)
+        d = np.asarray(dpids, dtype=np.uint64)
         i = np.searchsorted(self.dpids, d)
         i = np.minimum(i, self.V - 1)
         ok = self.dpids[i] == d
@@ -109,14 +112,23 @@ class CSR(object):
         return int(np.diff(self.row_ptr).max())
 
 
+def _dpid_array(x):
+    """dpids (Python ints up to 2**64 - 1, or an integer array) as uint64."""
+    if isinstance(x, np.ndarray):
+        if x.dtype.kind == "i" and x.size and int(x.min()) < 0:
+            raise ValueError("datapath ids are unsigned")
+        return x.astype(np.uint64)
+    return np.asarray(x, dtype=np.uint64)
+
+
 def build_csr(link_src, link_dst, link_sport, extra_vertices=()):
     """CSR from directed links in creation order (last duplicate wins)."""
-    src = np.asarray(link_src, dtype=np.int64)
-    dst = np.asarray(link_dst, dtype=np.int64)
+    src = _dpid_array(link_src)
+    dst = _dpid_array(link_dst)
     sport = np.asarray(link_sport, dtype=np.int64)
-    parts = [src, dst, np.asarray(list(extra_vertices), dtype=np.int64)]
+    parts = [src, dst, _dpid_array(list(extra_vertices))]
     dpids = np.unique(np.concatenate(parts)) if sum(p.size for p in parts) else \
-        np.zeros(0, np.int64)
+        np.zeros(0, np.uint64)
     V = dpids.shape[0]
     if src.size:
         si = np.searchsorted(dpids, src)

@@ -23,7 +23,7 @@ first route query raises (``sdnmpi_amd._native.NativeUnavailable`` /
 
 import numpy as np
 
-from ..engine import RouteEngine, TableCache, shortest_paths_lex, tree_path
+from ..engine import RouteEngine, TableCache, _host, _take, shortest_paths_lex, tree_path
 from ..graph import TrackedDict, Versions, export_graph
 from ..incremental import edge_diff
 
@@ -41,7 +41,12 @@ class TopologyDB(object):
     """Reference-compatible topology store with GPU route tables.
 
     ``engine``: a :class:`~sdnmpi_amd.engine.RouteEngine` to share between
-    databases (default: one on HIP device ``device``, created lazily).
+    databases (default: one on HIP device ``device`` -- or, with
+    ``devices=[...]``, one context over several GPUs of the node with the
+    sources sharded across them -- created lazily).
+    ``table_budget``: bytes of device tables kept per route mode (default
+    ``engine.DEFAULT_TABLE_BUDGET``); beyond it the oldest rows are evicted
+    and batches shrink to what fits.
     ``batch_sources``: when a table must be computed, compute it for every
     host-bearing switch at once (the all-pairs batch) instead of only the
     switch asked about.
@@ -50,11 +55,13 @@ class TopologyDB(object):
     recompute only the others.
     """
 
-    def __init__(self, engine=None, device=0, batch_sources=True, incremental=True):
+    def __init__(self, engine=None, device=0, batch_sources=True, incremental=True,
+                 devices=None, table_budget=None):
         super(TopologyDB, self).__init__()
         self._versions = Versions()
         self._engine = engine
-        self._device = device
+        self._device = list(devices) if devices else device
+        self._budget = table_budget
         self._batch = batch_sources
         self._incremental = incremental
         self._export = None
@@ -141,7 +148,7 @@ class TopologyDB(object):
             else:
                 old = self._cache
                 self._export = ex = new
-                self._cache = TableCache(new)
+                self._cache = TableCache(new, self._budget)
                 if self._incremental and old is not None:
                     diff = edge_diff(old.export.csr, new.csr)
                     if diff is not None:
@@ -156,16 +163,21 @@ class TopologyDB(object):
         return self._hv[1]
 
     def _dfs(self, ex, s):
+        """(parent, port) host rows of source s (one row copied back from
+        the device tables, kept in a small host cache)."""
         c = self._cache
-        batch = self._host_vertices(ex) if self._batch and s not in c.dfs_row else ()
-        tabs = c.dfs_rows(self.engine, [s], batch)
-        r = c.dfs_row[s]
-        return tabs[0][r], tabs[1][r]
+        if s not in c.dfs:
+            batch = self._host_vertices(ex) if self._batch else ()
+            c.dfs_rows(self.engine, [s], batch)
+        row = c.dfs.host_row(s)
+        return row[0], row[1]
 
     def _dist(self, ex, d):
-        batch = self._host_vertices(ex) if self._batch and d not in self._cache.sp_row else ()
-        tabs = self._cache.sp_rows(self.engine, [d], batch)
-        return tabs[0][self._cache.sp_row[d]]
+        c = self._cache
+        if d not in c.sp:
+            batch = self._host_vertices(ex) if self._batch else ()
+            c.sp_rows(self.engine, [d], batch)
+        return c.sp.host_row(d)[0]
 
     # -- route lookup (topology_db.py:124-188) ---------------------------
     def _mac_to_int(self, mac):
@@ -257,21 +269,28 @@ class TopologyDB(object):
         dict(sources, parent, port, hops, dpids);  ``mode="shortest"``:
         per-destination dict(destinations, dist, nh, nh_port, dpids).
         """
+        if mode not in ("dfs", "shortest"):
+            raise ValueError("mode must be 'dfs' or 'shortest'")
         ex = self.graph()
         hv = self._host_vertices(ex)
+        c = self._cache
+        store = c.dfs if mode == "dfs" else c.sp
+        get = c.dfs_rows if mode == "dfs" else c.sp_rows
+        parts = []                    # host copies, a budget's worth of rows at a time
+        step = store.cap() if store.row_bytes else len(hv)
+        for i in range(0, len(hv), max(1, step)):
+            chunk = hv[i:i + max(1, step)]
+            tabs = get(self.engine, chunk)
+            idx = np.asarray([store.row[v] for v in chunk], np.int64)
+            parts.append(tuple(_host(_take(a, idx)) for a in tabs))
+        cols = [np.concatenate([p[k] for p in parts]) if parts else None for k in range(3)]
         if mode == "dfs":
-            tabs = self._cache.dfs_rows(self.engine, hv)
-            rows = [self._cache.dfs_row[v] for v in hv]
-            return {"sources": np.asarray(hv, np.int32), "parent": tabs[0][rows],
-                    "port": tabs[1][rows], "hops": tabs[2][rows],
-                    "dpids": ex.csr.dpids}
-        if mode == "shortest":
-            tabs = self._cache.sp_rows(self.engine, hv)
-            rows = [self._cache.sp_row[v] for v in hv]
-            return {"destinations": np.asarray(hv, np.int32), "dist": tabs[0][rows],
-                    "nh": tabs[1][rows], "nh_port": tabs[2][rows],
-                    "dpids": ex.csr.dpids}
-        raise ValueError("mode must be 'dfs' or 'shortest'")
+            return {"sources": np.asarray(hv, np.int32), "parent": cols[0],
+                    "port": cols[1], "hops": cols[2], "dpids": ex.csr.dpids}
+        dist = cols[0].view(np.uint16) if cols[0] is not None and cols[0].dtype == np.int16 \
+            else cols[0]
+        return {"destinations": np.asarray(hv, np.int32), "dist": dist,
+                "nh": cols[1], "nh_port": cols[2], "dpids": ex.csr.dpids}
 
     def _find_routes_multiple(self, pairs):
         """find_route(a, b, multiple=True) for many pairs: per-destination
@@ -292,17 +311,21 @@ class TopologyDB(object):
         if not want:
             return out
         batch = self._host_vertices(ex) if self._batch else ()
-        tabs = self._cache.sp_rows(self.engine, sorted(set(want)), batch)
-        dist = tabs[0]
-        idx = [i for i in range(n) if ends[i] is not None]
-        rows = [self._cache.sp_row[ends[i][1]] for i in idx]
-        srcs = [ends[i][0] for i in idx]
-        # only the destination rows these pairs use go to the GPU
-        urows, inv = np.unique(np.asarray(rows, np.int64), return_inverse=True)
-        sets = self.engine.ecmp(ex, dist[urows], inv, srcs)
-        for i, seqs in zip(idx, sets):
-            last = ends[i][2]
-            out[i] = [self._seq_fdb(ex, [int(v) for v in q], last) for q in seqs]
+        idx_all = [i for i in range(n) if ends[i] is not None]
+        uniq = sorted(set(want))
+        step = max(1, self._cache.sp.cap() - 1) if self._cache.sp.row_bytes else len(uniq)
+        for c0 in range(0, len(uniq), step):          # a budget's worth of rows at a time
+            chunk = set(uniq[c0:c0 + step])
+            tabs = self._cache.sp_rows(self.engine, sorted(chunk), batch if c0 == 0 else ())
+            idx = [i for i in idx_all if ends[i][1] in chunk]
+            rows = [self._cache.sp_row[ends[i][1]] for i in idx]
+            srcs = [ends[i][0] for i in idx]
+            # only the destination rows these pairs use go to the GPU
+            urows, inv = np.unique(np.asarray(rows, np.int64), return_inverse=True)
+            sets = self.engine.ecmp(ex, _take(tabs[0], urows), inv, srcs)
+            for i, seqs in zip(idx, sets):
+                last = ends[i][2]
+                out[i] = [self._seq_fdb(ex, [int(v) for v in q], last) for q in seqs]
         return out
 
     def route_entries(self, pairs):
@@ -334,13 +357,32 @@ class TopologyDB(object):
             return off, np.zeros(0, np.int64), np.zeros(0, np.int32)
         want = sorted(set(sv[ok].tolist()))
         batch = self._host_vertices(ex) if self._batch else ()
-        tabs = self._cache.dfs_rows(self.engine, want, batch)
-        rows = np.asarray([self._cache.dfs_row[v] for v in sv[ok].tolist()], np.int32)
-        o, sw, hp = self.engine.expand(ex, tabs, rows, dv[ok], last[ok])
+        c = self._cache
+        step = max(1, c.dfs.cap() - 1) if c.dfs.row_bytes else len(want)
         lens = np.zeros(n, np.int64)
-        lens[ok] = np.diff(o)
+        pieces = []                   # (pair ids, offsets, switches, ports) per source chunk
+        for c0 in range(0, len(want), step):        # a budget's worth of sources at a time
+            chunk = want[c0:c0 + step]
+            tabs = c.dfs_rows(self.engine, chunk, batch if c0 == 0 else ())
+            mine = ok[np.isin(sv[ok], np.asarray(chunk, np.int64))]
+            rows = np.asarray([c.dfs_row[v] for v in sv[mine].tolist()], np.int32)
+            o, sw, hp = self.engine.expand(ex, tabs, rows, dv[mine], last[mine])
+            lens[mine] = np.diff(o)
+            pieces.append((mine, o, sw, hp))
         np.cumsum(lens, out=off[1:])
-        return off, ex.csr.dpids[sw], hp
+        total = int(off[-1])
+        sw_all = np.zeros(total, np.int64)
+        hp_all = np.zeros(total, np.int32)
+        for mine, o, sw, hp in pieces:
+            if len(pieces) == 1 and mine.size == n:
+                sw_all, hp_all = sw, hp
+                break
+            dst0 = off[mine]                      # pair starts in the full output
+            ln = np.diff(o)
+            pos = np.repeat(dst0 - o[:-1], ln) + np.arange(int(o[-1]))
+            sw_all[pos] = sw
+            hp_all[pos] = hp
+        return off, ex.csr.dpids[np.asarray(sw_all, np.int64)], hp_all
 
     def find_routes(self, pairs, multiple=False):
         """find_route over many (src_mac, dst_mac) pairs; tables are computed
@@ -361,7 +403,8 @@ class TopologyDB(object):
                 ep = self._endpoint(a)
                 if ep is not None:
                     want.add(ex.index[ep[0]])
-            self._cache.dfs_rows(self.engine, sorted(want), self._host_vertices(ex))
+            if len(want) < self._cache.dfs.cap():
+                self._cache.dfs_rows(self.engine, sorted(want), self._host_vertices(ex))
         return [self.find_route(a, b, multiple) for a, b in pairs]
 
 

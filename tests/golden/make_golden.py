@@ -239,8 +239,12 @@ def scenarios(TopologyDB):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--small", action="store_true")
+    ap.add_argument("--large-only", action="store_true",
+                    help="regenerate only the full-size samples")
     args = ap.parse_args()
     TopologyDB = import_reference()
+    if args.large_only:
+        return large(TopologyDB)
 
     scenarios(TopologyDB)
     run_fabric(TopologyDB, "mock", T.mock_square(), multiple=True)
@@ -260,16 +264,21 @@ def main():
                multiple=True)
     if args.small:
         return
+    large(TopologyDB)
+
+
+def large(TopologyDB):
     # full-size BASELINE configs: sampled host pairs (the reference needs
-    # 2.9 ms/pair at k=48 and ~1-4 s/pair on the torus and Jellyfish)
+    # 2.9 ms/pair at k=48 and ~1-4 s/pair on the torus and Jellyfish; the
+    # seeded sequences extend the round-1 samples, whose pairs come first)
     run_fabric(TopologyDB, "fat_tree_k48_sample", T.fat_tree(48),
                store_fabric=False, n_sample=400, seed=48)
     run_fabric(TopologyDB, "dragonfly_a16_h8_p8_sample", T.dragonfly(16, 8, 8),
                store_fabric=False, n_sample=200, seed=16)
     run_fabric(TopologyDB, "torus_32x32x32_sample", T.torus3d(32, 32, 32),
-               store_fabric=False, n_sample=6, seed=32)
+               store_fabric=False, n_sample=72, seed=32)
     run_fabric(TopologyDB, "jellyfish_n100000_r16_sample",
-               T.jellyfish(100000, 16, seed=1), store_fabric=False, n_sample=4,
+               T.jellyfish(100000, 16, seed=1), store_fabric=False, n_sample=40,
                seed=100)
 
 

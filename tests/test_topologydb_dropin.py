@@ -408,3 +408,58 @@ def test_edge_port_helpers_match_reference_loop():
     check()
     del db.links[lk.dst.dpid]
     check()
+
+
+@pytest.mark.parametrize("budget_rows", [1, 3, 7])
+def test_table_budget_eviction_fake_engine(budget_rows):
+    """A table budget of a few rows: batches shrink, old rows are evicted,
+    route_entries / find_routes(multiple=True) / route_tables run in chunks of
+    sources -- and every answer still equals the reference semantics."""
+    from oracle import oracle as O
+    from sdnmpi_amd import topologies as T
+    fabric = T.fat_tree(4)
+    V = fabric.csr().V
+    db = fabric.populate(TopologyDB(table_budget=budget_rows * 3 * 4 * V))
+    eng = _FakeEngine()
+    db._engine = eng
+    macs = fabric.host_macs()
+    pairs = [(a, b) for a in macs for b in macs[::2]]
+    assert db.find_routes(pairs) == [O.find_route_pair(db, a, b) for a, b in pairs]
+    assert len(db._cache.dfs) <= budget_rows
+    for a, b in pairs[::7]:
+        assert db.find_route(a, b) == O.find_route_pair(db, a, b)
+    assert db.find_routes(pairs[:40], True) == \
+        [O.find_routes_all_shortest(db, a, b) for a, b in pairs[:40]]
+    assert len(db._cache.sp) <= max(1, budget_rows * 3 * 4 * V // (10 * V))
+    t = db.route_tables("dfs")
+    po, to, ho = O.dfs_tables(fabric.csr(), t["sources"])
+    np.testing.assert_array_equal(t["parent"], po)
+    np.testing.assert_array_equal(t["hops"], ho)
+    s = db.route_tables("shortest")
+    do, _, nhpo = O.dest_tables(fabric.csr(), s["destinations"])
+    np.testing.assert_array_equal(s["dist"], do)
+    np.testing.assert_array_equal(s["nh_port"], nhpo)
+
+
+def test_unsigned_64bit_dpids():
+    """Ryu datapath ids are unsigned 64-bit: dpids >= 2**63 sort and route as
+    the reference's Python ints do."""
+    from oracle import oracle as O
+    big = [2**63 + 5, 2**64 - 1, 7, 2**63]
+    db = TopologyDB()
+    db._engine = _FakeEngine()
+    for d in big:
+        db.add_switch(Switch(d))
+    for i, u in enumerate(big):
+        for j, v in enumerate(big):
+            if u != v and (i + j) % 3 != 0:
+                db.add_link(Link(Port(u, 10 + j), Port(v, 10 + i)))
+    macs = ["02:00:00:00:01:%02x" % i for i in range(len(big))]
+    for m, d in zip(macs, big):
+        db.add_host(Host(m, Port(d, 1)))
+    ex = db.graph()
+    assert [int(x) for x in ex.csr.dpids] == sorted(big)
+    for a in macs:
+        for b in macs:
+            assert db.find_route(a, b) == O.find_route_pair(db, a, b)
+            assert db.find_route(a, b, True) == O.find_routes_all_shortest(db, a, b)
