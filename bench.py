@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--layout", choices=["auto", "packed", "int32"], default="auto",
                     help="dfs tables: packed u32 (parent | port << 16) when the fabric "
                          "allows it (V <= 65535, 16-bit ports), else int32 parent + port")
+    ap.add_argument("--max-sources", type=int, default=0,
+                    help="dfs/shortest: only the first N sources/destinations (probes; the "
+                         "config then says so and value counts only their routes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0,
                     help="bound on the CPU baseline's work")
@@ -438,6 +441,9 @@ def main():
     srcs, counts = np.unique(hv, return_counts=True)
     srcs = srcs.astype(np.int32)
     H = fabric.n_hosts
+    if args.max_sources and args.max_sources < len(srcs):
+        pick = np.linspace(0, len(srcs) - 1, args.max_sources).astype(np.int64)
+        srcs, counts = srcs[pick], counts[pick]
     S = len(srcs)
     lo, hi, per = D.shard_bounds(S, world, rank)
     my = D.padded_shard(srcs, world, rank)   # pad: id -1 -> empty row
@@ -524,7 +530,7 @@ def main():
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
 
     ms_per_step = elapsed / args.steps * 1e3
-    routes = float(H) * float(H)                 # every host pair, every step
+    routes = float(counts.sum()) * float(H)      # every host pair of these sources
     value = routes / (ms_per_step / 1e3)
     bytes_launch = algorithmic_bytes_per_source(V, E, args.mode, packed) * (hi - lo)
     achieved = bytes_launch / (kern_ms / 1e3) / 1e9
@@ -558,6 +564,7 @@ def main():
                 "" if args.mode == "dfs" else "(multiple=True)[0] + dist"),
             "fabric": args.fabric, "V": V, "E": E, "hosts": H, "sources": S,
             "host_pairs_per_step": int(routes), "table_layout": layout,
+            "source_subset": bool(args.max_sources and S < len(np.unique(hv))),
             "parallelism": "sources sharded over %d GPU(s)%s" % (
                 world, " + RCCL all-gather of the tables (double-buffered: step i+1's "
                        "kernel overlaps step i's gather)" if world > 1 else ""),
