@@ -64,6 +64,8 @@ def parse():
                     help="dfs/shortest: only the first N sources/destinations (probes; the "
                          "config then says so and value counts only their routes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-flows", action="store_true",
+                    help="dfs mode: skip the materialised flow-entry rate of every host pair")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0,
                     help="bound on the CPU baseline's work")
     return ap.parse_args()
@@ -178,6 +180,64 @@ class _DictDB(object):
 
     def add_host(self, h):
         self.hosts[h.mac] = h
+
+
+def materialised_flows(ctx, dev, stream, csr, fabric, srcs, chunk=1 << 22):
+    """The fdb of EVERY host pair (Router._add_flows_for_path's input,
+    reference sdnmpi/router.py:83-104; _route_to_fdb, topology_db.py:127-138)
+    materialised in HBM from the default-route tables: the headline counts
+    pairs whose route the tables determine, this counts pairs whose flow
+    entries were actually written.  Requests (tree row, destination switch,
+    host port) of all H^2 pairs are built once, untimed; then chunks of
+    `chunk` pairs are sized (offsets) and expanded into a reused output
+    buffer, timed with HIP events on the kernels' stream."""
+    V, H = csr.V, fabric.n_hosts
+    hv, hp = fabric.host_table()
+    S = len(srcs)
+    t_src = torch.from_numpy(srcs).to(dev)
+    par = torch.empty((S, V), dtype=torch.int32, device=dev)
+    prt = torch.empty_like(par)
+    hop = torch.empty_like(par)
+    ctx.dfs_tables_device(t_src.data_ptr(), S, par.data_ptr(), prt.data_ptr(), hop.data_ptr())
+    ctx.synchronize()
+    max_len = int(hop.max().item()) + 1
+    row_of_host = torch.from_numpy(np.searchsorted(srcs, hv).astype(np.int32)).to(dev)
+    sw_of_host = torch.from_numpy(hv.astype(np.int32)).to(dev)
+    port_of_host = torch.from_numpy(hp.astype(np.int32)).to(dev)
+    npairs = H * H
+    off = torch.empty(chunk + 1, dtype=torch.int64, device=dev)
+    sw = torch.empty(chunk * max_len, dtype=torch.int32, device=dev)
+    hpo = torch.empty_like(sw)
+    reqs = []                                   # (rows, dsts, last) per chunk, untimed
+    for p0 in range(0, npairs, chunk):
+        idx = torch.arange(p0, min(npairs, p0 + chunk), dtype=torch.int64, device=dev)
+        a, b = idx // H, idx % H
+        reqs.append((row_of_host[a].contiguous(), sw_of_host[b].contiguous(),
+                     port_of_host[b].contiguous()))
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    entries = torch.zeros((), dtype=torch.int64, device=dev)
+    e0.record(stream)
+    for rows, dsts, last in reqs:
+        n = rows.shape[0]
+        ctx.route_offsets_device(hop.data_ptr(), rows.data_ptr(), dsts.data_ptr(), n,
+                                 off.data_ptr(), nrows=S)
+        ctx.expand_routes_device(par.data_ptr(), prt.data_ptr(), S, rows.data_ptr(),
+                                 dsts.data_ptr(), last.data_ptr(), n, off.data_ptr(),
+                                 sw.data_ptr(), hpo.data_ptr())
+        entries += off[n]                        # stream-ordered, no host sync
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ctx.synchronize()
+    ms = e0.elapsed_time(e1)
+    total = int(entries.item())
+    return {"value": npairs / (ms / 1e3), "unit": "routes/s", "pairs": npairs,
+            "entries": total, "entries_per_s": total / (ms / 1e3), "ms": ms,
+            "kernel": ctx.last_kernel(), "chunk_pairs": chunk,
+            "note": "flow entries (dpid, out_port) of all %d^2 host pairs written to HBM "
+                    "(offsets + route_jump expansion per %d-pair chunk, one reused output "
+                    "buffer), tables and requests resident; compare the headline, which "
+                    "counts pairs whose route the tables determine" % (H, chunk)}
 
 
 def main_flows(args, world, rank, local, dev):
@@ -597,6 +657,11 @@ def main():
             "value": routes / dt, "unit": "routes/s", "ms_per_call": dt * 1e3,
             "note": "sdnr_dfs_tables%s with host buffers (sources H2D, tables D2H, "
                     "synchronous), not the HBM-resident bench value" % ("_packed" if packed else "")}
+    # fat-trees only: their default routes are ~70 entries; a torus or
+    # Jellyfish all-pairs fdb set (~2,400-5,600 entries per pair) is TBs
+    if rank == 0 and world == 1 and args.mode == "dfs" and not args.max_sources and \
+            not args.no_flows and args.fabric.startswith("fat_tree"):
+        out["materialised_flows"] = materialised_flows(ctx, dev, stream, csr, fabric, srcs)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "dfs":
         base, ref = cpu_baseline(fabric, csr, srcs, counts, H, args.cpu_budget_s)
         out["cpu_baseline"] = base

@@ -74,6 +74,12 @@ static void free_graph(sdnr_ctx *c)
     if (c->radj16 && c->radj_owned) (void)hipFree(c->radj16);
     if (c->adj16) (void)hipFree(c->adj16);
     if (c->deg32) (void)hipFree(c->deg32);
+    if (c->adj32) (void)hipFree(c->adj32);
+    if (c->ell16) (void)hipFree(c->ell16);
+    if (c->ell_hi) (void)hipFree(c->ell_hi);
+    c->adj32 = nullptr;
+    c->ell16 = nullptr;
+    c->ell_hi = nullptr;
     c->adj16 = nullptr;
     c->radj16 = nullptr;
     c->deg32 = nullptr;
@@ -319,6 +325,34 @@ static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *
             free_graph(ctx);
             return rc;
         }
+        // narrow ELL ids for the large-graph DFS: u16 (V <= 65535: id 0xFFFF is
+        // free for padding), or 16 low bits + a per-row mask of bit 16
+        // (V <= 131071, rows <= 32 slots); padding decodes to an id >= V
+        if (V <= 131071 && W <= 32) {
+            std::vector<uint16_t> e16(ec.size() + kPad, (uint16_t)0xFFFF);
+            std::vector<uint32_t> hi(V > 65535 ? (size_t)V + kPad : 0, 0u);
+            for (size_t i = 0; i < ec.size(); ++i) {
+                const int32_t x = ec[i];
+                e16[i] = (uint16_t)(x < 0 ? 0xFFFF : (x & 0xFFFF));
+                if (V > 65535 && (x < 0 || (x >> 16)))
+                    hi[i / (size_t)W] |= 1u << (i % (size_t)W);
+            }
+            hipError_t he = hipMalloc(reinterpret_cast<void **>(&ctx->ell16), e16.size() * 2);
+            if (he == hipSuccess)
+                he = hipMemcpyAsync(ctx->ell16, e16.data(), e16.size() * 2, hipMemcpyHostToDevice,
+                                    ctx->stream);
+            if (he == hipSuccess && !hi.empty()) {
+                he = hipMalloc(reinterpret_cast<void **>(&ctx->ell_hi), hi.size() * 4);
+                if (he == hipSuccess)
+                    he = hipMemcpyAsync(ctx->ell_hi, hi.data(), hi.size() * 4,
+                                        hipMemcpyHostToDevice, ctx->stream);
+            }
+            if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
+            if (he != hipSuccess) {
+                free_graph(ctx);
+                return sdnr_hip_fail(he, "graph_upload(ell16)");
+            }
+        }
         SDNR_HIP(hipStreamSynchronize(ctx->stream));   // before ec/ep go away
     }
     // u16 rows of stride 64 (one 128-byte line) for the cooperative DFS
@@ -355,6 +389,14 @@ static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *
         hipError_t he = hipMalloc(reinterpret_cast<void **>(&ctx->adj16), rows * 2);
         if (he == hipSuccess)
             he = hipMemcpyAsync(ctx->adj16, a16.data(), rows * 2, hipMemcpyHostToDevice, ctx->stream);
+        std::vector<int32_t> a32;
+        if (he == hipSuccess && V <= 16384) {
+            a32.assign(a16.begin(), a16.end());
+            he = hipMalloc(reinterpret_cast<void **>(&ctx->adj32), rows * 4);
+            if (he == hipSuccess)
+                he = hipMemcpyAsync(ctx->adj32, a32.data(), rows * 4, hipMemcpyHostToDevice,
+                                    ctx->stream);
+        }
         if (he == hipSuccess && maxin <= SDNR_WAVE) {
             he = hipMalloc(reinterpret_cast<void **>(&ctx->deg32), d32.size() * 4);
             if (he == hipSuccess)

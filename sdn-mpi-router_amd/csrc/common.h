@@ -53,9 +53,13 @@ struct sdnr_ctx {
     int32_t W = 0;                      // ELL row width (0: CSR only)
     int32_t *row_ptr = nullptr, *col = nullptr, *port = nullptr;
     int32_t *ell_col = nullptr, *ell_port = nullptr;
+    uint16_t *ell16 = nullptr;          // ELL ids as u16 (low 16 bits when V > 65535), 0xFFFF pad
+    uint32_t *ell_hi = nullptr;         // per row: the 17th id bit of each slot (65535 <= V < 131071)
     uint16_t *adj16 = nullptr;          // (V+1) rows x 64 u16, sentinel V (V < 65535)
     uint16_t *radj16 = nullptr;         // in-neighbour rows, same layout (== adj16 if symmetric)
     uint32_t *deg32 = nullptr;          // out-degrees of 0..V (sentinel V: 0)
+    int32_t *adj32 = nullptr;           // adj16 widened to int32 (V <= 16384): rows the
+                                        // search wave prefetches land without a mask op
     bool radj_owned = false;
 
     // grow-only device scratch / staging

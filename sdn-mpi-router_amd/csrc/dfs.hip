@@ -1033,6 +1033,289 @@ __global__ __launch_bounds__(64) void dfs_global_packed_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Search / writer split for large graphs (torus 32^3, Jellyfish 100k).
+//
+// rocprofv3 on dfs_global_packed_kernel (profiles/r02_torus_dfs_*,
+// r02_jf_dfs_*): 84% / 64% of wave cycles waiting.  That kernel stores the
+// table entries (parent, port) from the search wave at every push, and a
+// wave's vector-memory counter is in order: the next row load's wait also
+// waits for every table store issued before it -- a write acknowledgement on
+// each step of the serial chain -- and the port lookup sits on the chain
+// too.  Here NS search waves of a workgroup (one source each) never store on
+// the chain: a push appends (vertex, parent, row slot[, depth]) records to
+// the wave's LDS queue and a writer wave drains the NS queues, loads the
+// ports and issues the table stores (parent | port << 16 directly when the
+// packed layout is asked for).  Rows are read in the narrowest format the
+// vertex count allows -- u16 ids below 65,535 vertices; 16 low bits plus a
+// per-row mask of the 17th bit below 131,071 (the 100k Jellyfish ELL drops
+// from 6.4 MB to 3.6 MB, inside an XCD's 4 MB L2).  The search itself is the
+// batched pop of dfs_global_packed_kernel (first live entry from the top).
+// ---------------------------------------------------------------------------
+constexpr int kRow32 = 0, kRow16 = 1, kRow17 = 2;
+constexpr int kSplitQ = 64;                    // queued records per search wave
+
+template <int FMT>
+__device__ __forceinline__ int split_row(const void *__restrict__ rows,
+                                         const uint32_t *__restrict__ rhi, int V, int W, int u,
+                                         int pos)
+{
+    const size_t e = (size_t)u * W + pos;
+    int x;
+    if (FMT == kRow32) {
+        x = static_cast<const int32_t *>(rows)[e];
+    } else {
+        x = (int)static_cast<const uint16_t *>(rows)[e];
+        if (FMT == kRow17) x |= (int)((rhi[u] >> pos) & 1u) << 16;
+    }
+    return x < V ? x : -1;                     // padding (-1, 0xFFFF, 0x1FFFF)
+}
+
+__host__ __device__ inline size_t split_lds_words(int V, int ring, int ns, bool hops)
+{
+    const size_t VWp = (size_t)((((V + 31) >> 5) + 3) & ~3);
+    return (size_t)ns * (VWp + 2 * (size_t)ring) + (size_t)ns * kSplitQ * (hops ? 3 : 2) +
+           ((3 * (size_t)ns + 3) & ~(size_t)3);
+}
+
+template <int LPR, int J, bool HOPS, int RING, int NS, int FMT, bool PACKED>
+__global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
+    int V, int W, const void *__restrict__ rows, const uint32_t *__restrict__ rhi,
+    const int32_t *__restrict__ ell_port, const int32_t *__restrict__ src, int nsrc,
+    int32_t *__restrict__ out_parent, int32_t *__restrict__ out_port,
+    int32_t *__restrict__ out_hops, uint2 *__restrict__ spill_all, int *__restrict__ err)
+{
+    constexpr int R = 64 / LPR;
+    constexpr int K = R * J;
+    constexpr unsigned kSpin = 1u << 22;
+    constexpr unsigned kIdle = 1u << 26;
+    static_assert(K <= 64, "one stack slot per lane");
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int VW = (V + 31) >> 5;
+    const int VWp = (VW + 3) & ~3;
+    const int per = VWp + 2 * RING;           // words per search wave: vis | stack ring
+    uint2 *qrec = reinterpret_cast<uint2 *>(lds + NS * per);
+    uint32_t *qdep = reinterpret_cast<uint32_t *>(qrec + NS * kSplitQ);
+    // ctl[k] records published by search wave k, ctl[NS + k] records the
+    // writer consumed, ctl[2NS + k] table row of wave k's source (-2 none
+    // yet, -1 no more)
+    int *ctl = reinterpret_cast<int *>(qdep + (HOPS ? NS * kSplitQ : 0));
+    const int lane = lane_id();
+    const int w = uniform((int)(threadIdx.x >> 6));
+    if (threadIdx.x < 3 * NS) ctl[threadIdx.x] = (int)threadIdx.x >= 2 * NS ? -2 : 0;
+    __syncthreads();
+
+    if (w < NS) {
+        // ------------------------------------------------------ a search wave
+        const int pos = lane % LPR;
+        const int sub = lane / LPR;
+        const uint64_t lowmask = (LPR == 64) ? ~0ull : ((1ull << LPR) - 1ull);
+        uint32_t *vis = lds + w * per;
+        uint2 *ring = reinterpret_cast<uint2 *>(vis + VWp);   // (v, depth)
+        uint2 *q = qrec + w * kSplitQ;
+        uint32_t *qd = qdep + w * kSplitQ;
+        const int slot_id = blockIdx.x * NS + w;
+        uint2 *spill = spill_all + (size_t)slot_id * (size_t)V;
+        int pub = 0, cons = 0;
+        for (int si = slot_id; si < nsrc; si += gridDim.x * NS) {
+            const int s = uniform(src[si]);
+            int32_t *prow = out_parent + (size_t)si * V;
+            int32_t *trow = PACKED ? nullptr : out_port + (size_t)si * V;
+            int32_t *hrow = HOPS ? out_hops + (size_t)si * V : nullptr;
+            if (s < 0 || s >= V) {                 // unknown source: empty row
+                for (int v = lane; v < V; v += SDNR_WAVE) {
+                    prow[v] = -1;                  // packed: 0xFFFFFFFF
+                    if (!PACKED) trow[v] = -1;
+                    if (HOPS) hrow[v] = -1;
+                }
+                continue;
+            }
+            for (int i = lane; i < VW; i += SDNR_WAVE) vis[i] = 0u;
+            if (lane == 0) {                       // the wave's LDS ops stay in order
+                vis[s >> 5] = 1u << (s & 31);
+                prow[s] = PACKED ? (int32_t)((uint32_t)s | 0xFFFF0000u) : s;
+                if (!PACKED) trow[s] = -1;
+                if (HOPS) hrow[s] = 0;
+                ring[0] = make_uint2((uint32_t)s, 0u);
+                __hip_atomic_store(&ctl[2 * NS + w], si, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            int lsp = 1, bot = 0, gsp = 0;
+            for (;;) {
+                if (lsp == 0) {
+                    if (gsp == 0) break;
+                    const int n = gsp < RING / 2 ? gsp : RING / 2;
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // own spill stores
+                    bot = (bot - n) & (RING - 1);
+                    for (int i = lane; i < n; i += SDNR_WAVE)
+                        ring[(bot + i) & (RING - 1)] = spill[gsp - n + i];
+                    gsp -= n;
+                    lsp = n;
+                }
+                const int kk = lsp < K ? lsp : K;
+                uint2 me = ring[(bot + lsp - 1 - lane) & (RING - 1)];
+                me.x = lane < kk ? me.x : 0u;
+                me.y = lane < kk ? me.y : 0u;
+                int x[J];
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                    const int slot = j * R + sub;
+                    const int u = __shfl((int)me.x, slot);           // slot >= kk: vertex 0
+                    x[j] = split_row<FMT>(rows, rhi, V, W, u, pos);
+                }
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                    const int ok = -(int)(((j * R + sub) < kk) & (pos < W));
+                    x[j] = (x[j] & ok) | ~ok;
+                }
+                uint64_t m[J];
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                    const int xi = x[j] & 0x7FFFFFFF;
+                    const uint32_t wv = vis[(xi >> 5) & ((x[j] >> 31) ^ -1)];
+                    m[j] = __ballot((x[j] >= 0) & (((wv >> (xi & 31)) & 1u) == 0u));
+                }
+                int jstar = J;
+#pragma unroll
+                for (int j = J - 1; j >= 0; --j)
+                    if (m[j] != 0) jstar = j;
+                if (jstar == J) {
+                    lsp -= kk;
+                    continue;
+                }
+                uint64_t mj = 0;
+                int vv = -1;
+#pragma unroll
+                for (int j = 0; j < J; ++j)
+                    if (j == jstar) {
+                        mj = m[j];
+                        vv = x[j];
+                    }
+                const int sstar = (__ffsll((unsigned long long)mj) - 1) / LPR;
+                const int istar = jstar * R + sstar;
+                const uint64_t mm = mj & (lowmask << (sstar * LPR));
+                const int eu = read_lane((int)me.x, istar);
+                const uint32_t ed = (uint32_t)read_lane((int)me.y, istar);
+                lsp -= istar + 1;
+                const int cnt = __popcll(mm);
+                // room in the record queue (the writer publishes its progress)
+                for (unsigned spin = 0; pub + cnt - cons > kSplitQ; ++spin) {
+                    cons = __hip_atomic_load(&ctl[NS + w], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (pub + cnt - cons <= kSplitQ) break;
+                    if (spin > kSpin) {
+                        if (lane == 0) atomicOr(err, 4);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (lsp + cnt > RING) {            // spill the oldest half
+                    for (int i = lane; i < RING / 2; i += SDNR_WAVE)
+                        spill[gsp + i] = ring[(bot + i) & (RING - 1)];
+                    gsp += RING / 2;
+                    bot = (bot + RING / 2) & (RING - 1);
+                    lsp -= RING / 2;
+                }
+                if ((mm >> lane) & 1ull) {
+                    const int rank = lanes_below(mm);
+                    atomicOr(&vis[vv >> 5], 1u << (vv & 31));
+                    q[(pub + rank) & (kSplitQ - 1)] =
+                        make_uint2((uint32_t)vv | ((uint32_t)pos << 26), (uint32_t)eu);
+                    if (HOPS) qd[(pub + rank) & (kSplitQ - 1)] = ed + 1u;
+                    ring[(bot + lsp + rank) & (RING - 1)] = make_uint2((uint32_t)vv, ed + 1u);
+                }
+                lsp += cnt;
+                pub += cnt;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                if (lane == 0) __hip_atomic_store(&ctl[w], pub, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            // this source's records drained before its row changes, then the
+            // entries of unreached vertices
+            for (unsigned spin = 0; cons != pub; ++spin) {
+                cons = __hip_atomic_load(&ctl[NS + w], __ATOMIC_ACQUIRE,
+                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (cons == pub) break;
+                if (spin > kSpin) {
+                    if (lane == 0) atomicOr(err, 8);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            for (int v = lane; v < V; v += SDNR_WAVE) {
+                if (((vis[v >> 5] >> (v & 31)) & 1u) == 0u) {
+                    prow[v] = -1;
+                    if (!PACKED) trow[v] = -1;
+                    if (HOPS) hrow[v] = -1;
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        if (lane == 0) __hip_atomic_store(&ctl[2 * NS + w], -1, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+        // ------------------------------------------------------ the writer
+        int consd[NS];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) consd[k] = 0;
+        unsigned idle = 0;
+        for (;;) {
+            bool any = false, all_done = true;
+#pragma unroll
+            for (int k = 0; k < NS; ++k) {
+                // records first, then the row: a source's row is announced
+                // before its first record, and changes only after the
+                // writer consumed all of the previous source's records
+                const int P = __hip_atomic_load(&ctl[k], __ATOMIC_ACQUIRE,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+                const int row = __hip_atomic_load(&ctl[2 * NS + k], __ATOMIC_ACQUIRE,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+                const int C = consd[k];
+                if (P > C) {
+                    any = true;
+                    all_done = false;
+                    const int n = P - C < SDNR_WAVE ? P - C : SDNR_WAVE;
+                    if (lane < n) {
+                        const int at = k * kSplitQ + ((C + lane) & (kSplitQ - 1));
+                        const uint2 r = qrec[at];
+                        const int v = (int)(r.x & 0x3FFFFFFu), slot = (int)(r.x >> 26);
+                        const int par = (int)r.y;
+                        const int pt = ell_port[(size_t)par * W + slot];
+                        const size_t e = (size_t)row * V + v;
+                        if (PACKED) {
+                            out_parent[e] = (int32_t)(((uint32_t)par & 0xFFFFu) |
+                                                      ((uint32_t)pt << 16));
+                        } else {
+                            out_parent[e] = par;
+                            out_port[e] = pt;
+                        }
+                        if (HOPS) out_hops[e] = (int)qdep[at];
+                    }
+                    consd[k] = C + n;
+                    // the record reads above are done (LDS ops in order)
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                    if (lane == 0) __hip_atomic_store(&ctl[NS + k], C + n, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else if (row != -1 ||
+                           __hip_atomic_load(&ctl[k], __ATOMIC_ACQUIRE,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP) != C) {
+                    all_done = false;              // running, or published meanwhile
+                }
+            }
+            if (all_done) break;
+            if (any) {
+                idle = 0;
+            } else {
+                if (++idle > kIdle) {
+                    if (lane == 0) atomicOr(err, 16);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Asynchronous counted pops (the k=48 headline kernel).
 //
 // Same counts as dfs_count_kernel, one observation further: a count may be
@@ -1052,9 +1335,19 @@ __global__ __launch_bounds__(64) void dfs_global_packed_kernel(
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int swz(int x) { return lds_swz(x); }   // common.h
 
-template <int NW, bool HOPS, bool PACKED>
+// lane's entry of u's 64-wide row, int32: a prefetched row can sit in its
+// register across the loop back-edge (a u16 row needs a zero-extension mask,
+// which the compiler places at the back-edge -- where it waits for the
+// prefetch to land and serialises the search again)
+template <typename AT>
+__device__ __forceinline__ int adjrow(const AT *__restrict__ adj, int u, int lane)
+{
+    return (int)adj[(size_t)u * 64 + lane];
+}
+
+template <int NW, bool HOPS, bool PACKED, typename AT = int32_t>
 __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
-    int V, const uint16_t *__restrict__ adj, const uint16_t *__restrict__ radj,
+    int V, const AT *__restrict__ adj, const uint16_t *__restrict__ radj,
     const uint32_t *__restrict__ deg, const int32_t *__restrict__ row_ptr,
     const int32_t *__restrict__ port, int W, const int32_t *__restrict__ ell_port,
     const int32_t *__restrict__ src, int nsrc, int32_t *__restrict__ out_parent,
@@ -1140,60 +1433,85 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             int pub = 1, pubd = 1, sp = 1, lo = 0;       // published / announced
             int pu0 = -1, pu1 = -1, xpre0 = V, xpre1 = V;   // rows of the two largest children
 #ifdef SDNR_STAMPS
-            unsigned long long st_t0, st_t1, st_row = 0, st_cand = 0, st_false = 0, st_bp = 0,
-                                               st_miss = 0, st_skip = 0, st_tc = 0, st_skipc = 0,
-                                               st_pushc = 0;
+            unsigned long long st_t0, st_t1, st_cand = 0, st_false = 0, st_bp = 0, st_miss = 0,
+                                               st_skip = 0, st_find = 0, st_row = 0, st_push = 0,
+                                               st_a, st_b, st_c;
             SDNR_STAMP(st_t0);
-            st_tc = st_t0;
+            st_c = st_t0;
 #endif
+            // children of the last push: their lanes of the row (kx), the
+            // fresh mask (km) and their counts (kc, gathered at the push,
+            // consumed one iteration later so the LDS round trip overlaps
+            // the row prefetch)
+            uint64_t km = 0;
+            int kx = V;
+            uint32_t kc = 0;
             for (;;) {
-                uint64_t m = 0;
-                int e = V;
-                while (sp > 0) {
-#ifdef SDNR_STAMPS
-                    st_skip++;
-#endif
-                    const int kk = sp < 64 ? sp : 64;
-                    const int at = sp - 1 - lane;
-                    e = stk[at < 0 ? 0 : at];
-                    e = lane < kk ? e : V;
-                    const uint32_t c = __hip_atomic_load(&cnt[swz(e)], __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
-                    m = __ballot(c != 0u);
-                    if (m) break;
-                    sp -= kk;
+                int u = -1;
+                if (km) {
+                    // the next pop is one of these children whenever one of
+                    // them has a non-zero count: they are the top of the
+                    // stack, highest lane (largest id, pushed last) on top,
+                    // and every child above the first live one is a leaf pop
+                    const uint64_t live = __ballot(kc != 0u) & km;
+                    if (live) {
+                        const int top = highest_lane(live);
+                        u = read_lane(kx, top);
+                        const uint64_t above = top == 63 ? 0ull : km & (~0ull << (top + 1));
+                        sp -= __popcll(above) + 1;
+                    } else {
+                        sp -= __popcll(km);       // all of them leaf pops
+                    }
+                    km = 0;
                 }
-                // publish the previous push's children now: the skip's LDS
-                // reads have waited for those writes, so the release is free
+                if (u < 0) {
+                    uint64_t m = 0;
+                    int e = V;
+                    while (sp > 0) {
+#ifdef SDNR_STAMPS
+                        st_skip++;
+#endif
+                        const int kk = sp < 64 ? sp : 64;
+                        const int at = sp - 1 - lane;
+                        e = stk[at < 0 ? 0 : at];
+                        e = lane < kk ? e : V;
+                        const uint32_t c = __hip_atomic_load(&cnt[swz(e)], __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+                        m = __ballot(c != 0u);
+                        if (m) break;
+                        sp -= kk;
+                    }
+                    if (m) {
+                        const int first = __ffsll((unsigned long long)m) - 1;
+                        u = read_lane(e, first);
+                        sp -= first + 1;
+                    }
+                }
+                // publish the previous push's children: LDS-only release (the
+                // ring lives in LDS; a full fence would also wait for the row
+                // prefetches still in flight)
                 if (pub != pubd) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
                     if (lane == 0) __hip_atomic_store(&ctl[0], pub, __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_WORKGROUP);
                     pubd = pub;
                 }
-                if (!m) break;
-                const int first = __ffsll((unsigned long long)m) - 1;
-                const int u = read_lane(e, first);
-                sp -= first + 1;
+                if (u < 0) break;
 #ifdef SDNR_STAMPS
-                unsigned long long ta, tb;
-                SDNR_STAMP(ta);
-                st_skipc += ta - st_tc;
                 if (u != pu0 && u != pu1) st_miss++;
+                st_cand++;
+                SDNR_STAMP(st_a);
+                st_find += st_a - st_c;
 #endif
-                const int x = (u == pu0) ? xpre0 : (u == pu1) ? xpre1
-                                                              : (int)adj[(size_t)u * 64 + lane];
+                const int x = (u == pu0) ? xpre0 : (u == pu1) ? xpre1 : adjrow(adj, u, lane);
                 const uint32_t wv = vis[x >> 5];
                 const bool fresh = ((wv >> (x & 31)) & 1u) == 0u;
                 const uint64_t mm = __ballot(fresh);
 #ifdef SDNR_STAMPS
-                SDNR_STAMP(tb);
-                st_row += tb - ta;
-                st_cand++;
                 if (mm == 0) st_false++;
-#endif
-#ifdef SDNR_STAMPS
-                if (mm == 0) st_tc = tb;
+                SDNR_STAMP(st_b);
+                st_row += st_b - st_a;
+                st_c = st_b;
 #endif
                 if (mm == 0) continue;           // stale count: a leaf pop after all
                 const int c = __popcll(mm);
@@ -1202,8 +1520,13 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                 pu0 = read_lane(x, highest_lane(mm));
                 const uint64_t rest = mm & ~(1ull << highest_lane(mm));
                 pu1 = rest ? read_lane(x, highest_lane(rest)) : -1;
-                xpre0 = adj[(size_t)pu0 * 64 + lane];
-                xpre1 = adj[(size_t)(rest ? pu1 : V) * 64 + lane];
+                xpre0 = adjrow(adj, pu0, lane);
+                xpre1 = adjrow(adj, rest ? pu1 : V, lane);
+                // the children's counts, for the next iteration
+                kc = fresh ? __hip_atomic_load(&cnt[swz(x)], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP) : 0u;
+                km = mm;
+                kx = x;
                 int du = 0;
                 if (HOPS) du = uniform((int)dep[u]);
                 // back-pressure: ring slots below every worker's progress are
@@ -1234,8 +1557,8 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                 pub += c;
                 sp += c;
 #ifdef SDNR_STAMPS
-                SDNR_STAMP(st_tc);
-                st_pushc += st_tc - tb;
+                SDNR_STAMP(st_c);
+                st_push += st_c - st_b;
 #endif
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1244,13 +1567,13 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             SDNR_STAMP(st_t1);
             if (lane == 0) {
                 atomicAdd(&g_stamp[0], st_t1 - st_t0);   // search wave lifetime
-                atomicAdd(&g_stamp[1], st_row);          // row + gather cycles
+                atomicAdd(&g_stamp[1], st_row);          // candidate -> row + visited ballot
                 atomicAdd(&g_stamp[2], st_cand);         // candidates popped
                 atomicAdd(&g_stamp[3], st_false);        // ... with no fresh child
                 atomicAdd(&g_stamp[4], st_bp);           // back-pressure sleeps
                 atomicAdd(&g_stamp[5], st_skip * 1000000ull + st_miss);   // skips, prefetch misses
-                atomicAdd(&g_stamp[6], st_skipc);        // skip cycles
-                atomicAdd(&g_stamp[7], st_pushc);        // push+publish cycles
+                atomicAdd(&g_stamp[6], st_find);         // loop top -> candidate found
+                atomicAdd(&g_stamp[7], st_push);         // push (non-false candidates)
             }
 #endif
         } else {
@@ -1564,6 +1887,99 @@ static int dfs_batch_depth(const sdnr_ctx *ctx)
     return ctx->max_deg >= 12 ? 16 : 8;
 }
 
+// SDNROUTE_DFS_SPLIT=0 keeps the single-wave lane-packed kernel (A/B, tests)
+static bool split_ok()
+{
+    const char *f = getenv("SDNROUTE_DFS_SPLIT");
+    return !(f && !strcmp(f, "0"));
+}
+
+// search / writer split kernel (large graphs, rows of <= 32 slots); records
+// the end event itself
+template <int NS>
+static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, int32_t *d_parent,
+                           int32_t *d_port, int32_t *d_hops, uint32_t *d_tree);
+
+// search waves per workgroup: 7 on sparse tori (4 workgroups of 8 waves fill
+// a CU's 32 wave slots with 28 sources), else 3 (LDS-bound: Jellyfish fits 3
+// workgroups of 3 sources); SDNROUTE_DFS_SPLIT_NS=3|7 overrides
+static int launch_split(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, int32_t *d_parent,
+                        int32_t *d_port, int32_t *d_hops, uint32_t *d_tree)
+{
+    int ns = ctx->W <= 8 && packed_j8(ctx->V) == 1 ? 7 : 3;
+    if (const char *f = getenv("SDNROUTE_DFS_SPLIT_NS")) {
+        const int k = atoi(f);
+        if (k == 3 || k == 7) ns = k;
+    }
+    return ns == 7 ? launch_split_ns<7>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree)
+                   : launch_split_ns<3>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree);
+}
+
+template <int NS>
+static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, int32_t *d_parent,
+                           int32_t *d_port, int32_t *d_hops, uint32_t *d_tree)
+{
+    const int V = ctx->V, W = ctx->W;
+    const bool packed = d_tree != nullptr, hops = d_hops != nullptr;
+    const int lpr = W <= 8 ? 8 : (W <= 16 ? 16 : 32);
+    const int j8 = packed_j8(V);
+    // stack ring: 128 entries on sparse tori (more sources per CU), 512 for
+    // rows of 9-32 slots (Jellyfish: 3 workgroups of 3 sources per CU)
+    const int ring = lpr == 8 ? (j8 == 1 ? 128 : 1024) : 512;
+    const int fmt = ctx->ell16 && V <= 65535 ? kRow16 : (ctx->ell16 && ctx->ell_hi ? kRow17 : kRow32);
+    if (packed && fmt != kRow16)
+        return sdnr_fail(SDNR_ERR_INVAL, "dfs split: packed tables need V <= 65535");
+    const size_t lds = split_lds_words(V, ring, NS, hops) * 4;
+    if (lds > SDNR_MAX_LDS_PER_BLOCK)
+        return sdnr_fail(SDNR_ERR_INVAL, "graph too large for the LDS visited sets (V=%d)", V);
+    size_t bpc = SDNR_LDS_PER_CU / lds;
+    if (bpc > (size_t)(32 / (NS + 1))) bpc = 32 / (NS + 1);    // 32 wave slots per CU
+    if (bpc < 1) bpc = 1;
+    int grid = (int)((size_t)ctx->num_cus * bpc);
+    const int need = (nsrc + NS - 1) / NS;
+    if (grid > need) grid = need;
+    int rc = sdnr_reserve(&ctx->scratch, &ctx->scratch_bytes,
+                          (size_t)grid * NS * (size_t)V * sizeof(uint2));
+    if (rc) return rc;
+    uint2 *spill = static_cast<uint2 *>(ctx->scratch);
+    const void *rows = fmt == kRow32 ? static_cast<const void *>(ctx->ell_col)
+                                     : static_cast<const void *>(ctx->ell16);
+    int32_t *par = packed ? reinterpret_cast<int32_t *>(d_tree) : d_parent;
+    static const char *names[3][2] = {{"dfs_split_kernel<row32>", "dfs_split_kernel<row32>"},
+                                      {"dfs_split_kernel<row16>", "dfs_split_kernel<row16,packed>"},
+                                      {"dfs_split_kernel<row17>", "dfs_split_kernel<row17>"}};
+    ctx->last_kernel = names[fmt][packed ? 1 : 0];
+#define SDNR_SPLIT(L_, J_, R_, H_, F_, P_)                                                    \
+    do {                                                                                     \
+        auto k = dfs_split_kernel<L_, J_, H_, R_, NS, F_, P_>;                               \
+        sdnr_allow_lds(reinterpret_cast<const void *>(k), lds);                              \
+        hipLaunchKernelGGL(k, dim3(grid), dim3((NS + 1) * 64), lds, ctx->stream, V, W, rows, \
+                           ctx->ell_hi, ctx->ell_port, d_src, nsrc, par, d_port, d_hops,     \
+                           spill, ctx->d_err);                                               \
+    } while (0)
+#define SDNR_SPLIT_F(L_, J_, R_, H_)                                                          \
+    do {                                                                                     \
+        if (fmt == kRow16 && packed) SDNR_SPLIT(L_, J_, R_, H_, kRow16, true);               \
+        else if (fmt == kRow16) SDNR_SPLIT(L_, J_, R_, H_, kRow16, false);                   \
+        else if (fmt == kRow17) SDNR_SPLIT(L_, J_, R_, H_, kRow17, false);                   \
+        else SDNR_SPLIT(L_, J_, R_, H_, kRow32, false);                                      \
+    } while (0)
+#define SDNR_SPLIT_H(L_, J_, R_)                                                              \
+    do {                                                                                     \
+        if (hops) SDNR_SPLIT_F(L_, J_, R_, true); else SDNR_SPLIT_F(L_, J_, R_, false);      \
+    } while (0)
+    if (lpr == 8 && ring == 128) SDNR_SPLIT_H(8, 1, 128);
+    else if (lpr == 8) SDNR_SPLIT_H(8, 2, 1024);
+    else if (lpr == 16) SDNR_SPLIT_H(16, 4, 512);
+    else SDNR_SPLIT_H(32, 8, 512);
+#undef SDNR_SPLIT_H
+#undef SDNR_SPLIT_F
+#undef SDNR_SPLIT
+    SDNR_HIP(hipGetLastError());
+    if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+    return SDNR_OK;
+}
+
 int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
                     int32_t *d_parent, int32_t *d_port, int32_t *d_hops, uint32_t *d_tree)
 {
@@ -1608,8 +2024,12 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
     const char *force = getenv("SDNROUTE_DFS_STRATEGY");
     const bool count_ok = ctx->adj16 != nullptr && ctx->radj16 != nullptr && V < 65535 &&
                           dfs_lds_bytes_count(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;
-    const bool async_ok = count_ok && dfs_lds_bytes_async(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;
+    const bool async_ok = count_ok && ctx->adj32 != nullptr &&
+                          dfs_lds_bytes_async(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;
     const bool async = async_ok && (force ? !strcmp(force, "async") : small);
+    if (!async && !small && ell && ctx->W <= 32 && packed_ok() && split_ok() &&
+        (!packed || (ctx->ell16 && V <= 65535)))
+        return launch_split(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree);
     if (packed && !async) {
         // no packed epilogue in this strategy: int32 tables into scratch, then pack
         const size_t n = (size_t)nsrc * (size_t)V;
@@ -1644,14 +2064,31 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
     do {                                                                                     \
         auto k = dfs_async_kernel<N_, H_, P_>;                                               \
         allow_full_lds(k);                                                                   \
-        hipLaunchKernelGGL(k, dim3(cgrid), dim3(N_ * 64), cl, ctx->stream, V, ctx->adj16,    \
+        hipLaunchKernelGGL(k, dim3(cgrid), dim3(N_ * 64), cl, ctx->stream, V, ctx->adj32,    \
                            ctx->radj16, ctx->deg32, ctx->row_ptr, ctx->port, ctx->W,         \
                            ctx->ell_port, d_src, nsrc,                                       \
                            P_ ? reinterpret_cast<int32_t *>(d_tree) : d_parent, d_port,      \
                            d_hops, err);                                                     \
     } while (0)
 #define SDNR_ASYNC(N_, H_) SDNR_ASYNC_P(N_, H_, false)
-        if (packed) {
+        const char *r16 = getenv("SDNROUTE_DFS_ROW16");      // A/B: u16 search rows
+        if (r16 && !strcmp(r16, "1") && nw == 4) {
+            ctx->last_kernel = packed ? "dfs_async_kernel<4,packed,row16>" : "dfs_async_kernel<4,row16>";
+#define SDNR_ASYNC16(H_, P_)                                                                 \
+    do {                                                                                     \
+        auto k = dfs_async_kernel<4, H_, P_, uint16_t>;                                      \
+        allow_full_lds(k);                                                                   \
+        hipLaunchKernelGGL(k, dim3(cgrid), dim3(4 * 64), cl, ctx->stream, V, ctx->adj16,     \
+                           ctx->radj16, ctx->deg32, ctx->row_ptr, ctx->port, ctx->W,         \
+                           ctx->ell_port, d_src, nsrc,                                       \
+                           P_ ? reinterpret_cast<int32_t *>(d_tree) : d_parent, d_port,      \
+                           d_hops, err);                                                     \
+    } while (0)
+            if (packed) SDNR_ASYNC16(false, true);
+            else if (hops) SDNR_ASYNC16(true, false);
+            else SDNR_ASYNC16(false, false);
+#undef SDNR_ASYNC16
+        } else if (packed) {
             static const char *pnames[] = {"", "", "dfs_async_kernel<2,packed>",
                                            "dfs_async_kernel<3,packed>",
                                            "dfs_async_kernel<4,packed>",

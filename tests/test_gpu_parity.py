@@ -35,6 +35,9 @@ def _strategy(monkeypatch, dfs=None, ell=None):
     if dfs == "global-nopack":
         monkeypatch.setenv("SDNROUTE_DFS_PACKED", "0")
         dfs = "global"
+    if dfs == "global-nosplit":                  # single-wave lane-packed kernel
+        monkeypatch.setenv("SDNROUTE_DFS_SPLIT", "0")
+        dfs = "global"
     if dfs:
         monkeypatch.setenv("SDNROUTE_DFS_STRATEGY", dfs)
     if ell is not None:
@@ -64,7 +67,7 @@ def _check_pairs(g, fabric, p, t, srcs):
 
 
 @pytest.mark.parametrize("strategy", ["auto", "async", "count", "coop", "lds", "global",
-                                      "global-ring128", "global-nopack"])
+                                      "global-ring128", "global-nopack", "global-nosplit"])
 @pytest.mark.parametrize("ell", [True, False])
 @pytest.mark.parametrize("name", G.SMALL)
 def test_dfs_small_all_sources(ctx, monkeypatch, name, strategy, ell):
@@ -81,7 +84,7 @@ def _pack(p, t):
     return ((p.astype(np.int64) & 0xFFFF) | ((t.astype(np.int64) & 0xFFFF) << 16)).astype(np.uint32)
 
 
-@pytest.mark.parametrize("strategy", ["auto", "lds", "global"])
+@pytest.mark.parametrize("strategy", ["auto", "lds", "global", "global-nosplit"])
 @pytest.mark.parametrize("name", ["mock", "fat_tree_k8", "dragonfly_a4_h2_p2", "random_V40",
                                   "jellyfish_n60_r5", "torus_5x3x2"])
 def test_dfs_packed_small(ctx, monkeypatch, name, strategy):
@@ -149,9 +152,14 @@ def test_dfs_fullsize_all_host_sources(ctx, name):
     _check_pairs(g, fabric, p, t, srcs)
 
 
+@pytest.mark.parametrize("split", ["1", "0", "ns3", "ns7"])
 @pytest.mark.parametrize("name,nsample", [("torus_32x32x32_sample", 384),
                                           ("jellyfish_n100000_r16_sample", 48)])
-def test_dfs_fullsize_sampled_sources(ctx, name, nsample):
+def test_dfs_fullsize_sampled_sources(ctx, monkeypatch, name, nsample, split):
+    if split.startswith("ns"):                   # search waves per workgroup
+        monkeypatch.setenv("SDNROUTE_DFS_SPLIT_NS", split[2:])
+    else:
+        monkeypatch.setenv("SDNROUTE_DFS_SPLIT", split)
     g = G.Golden(name)
     fabric = g.fabric()
     csr = fabric.csr()
@@ -514,3 +522,26 @@ def test_ecmp_counts_vs_level_dp(ctx, case):
         np.testing.assert_array_equal(paths[i], _count_dp(csr, dist[i]))
     if case == "ladder":
         assert int(paths[0, csr.V - 1]) == 2**64 - 1
+
+
+@pytest.mark.parametrize("packed", [True, False])
+@pytest.mark.parametrize("name", ["fat_tree_k8", "jellyfish_n60_r5", "torus_5x3x2", "random_V40",
+                                  "dragonfly_a4_h2_p2"])
+def test_dfs_async_row16(ctx, monkeypatch, name, packed):
+    """The async kernel with u16 search rows (A/B variant of the int32 rows)."""
+    _strategy(monkeypatch, "async")
+    monkeypatch.setenv("SDNROUTE_DFS_ROW16", "1")
+    csr = G.Golden(name).fabric().csr()
+    srcs = np.arange(csr.V, dtype=np.int32)
+    ctx.upload(csr)
+    po, to, ho = O.dfs_tables(csr, srcs, nthreads=NTHREADS)
+    if packed:
+        tree = ctx.dfs_tables_packed(srcs)
+        assert ctx.last_kernel() == "dfs_async_kernel<4,packed,row16>"
+        np.testing.assert_array_equal(tree, _pack(po, to))
+    else:
+        p, t, h = ctx.dfs_tables(srcs)
+        assert ctx.last_kernel() == "dfs_async_kernel<4,row16>"
+        np.testing.assert_array_equal(p, po)
+        np.testing.assert_array_equal(t, to)
+        np.testing.assert_array_equal(h, ho)
