@@ -74,10 +74,8 @@ static void free_graph(sdnr_ctx *c)
     if (c->radj16 && c->radj_owned) (void)hipFree(c->radj16);
     if (c->adj16) (void)hipFree(c->adj16);
     if (c->deg32) (void)hipFree(c->deg32);
-    if (c->adj32) (void)hipFree(c->adj32);
     if (c->ell16) (void)hipFree(c->ell16);
     if (c->ell_hi) (void)hipFree(c->ell_hi);
-    c->adj32 = nullptr;
     c->ell16 = nullptr;
     c->ell_hi = nullptr;
     c->adj16 = nullptr;
@@ -389,14 +387,6 @@ static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *
         hipError_t he = hipMalloc(reinterpret_cast<void **>(&ctx->adj16), rows * 2);
         if (he == hipSuccess)
             he = hipMemcpyAsync(ctx->adj16, a16.data(), rows * 2, hipMemcpyHostToDevice, ctx->stream);
-        std::vector<int32_t> a32;
-        if (he == hipSuccess && V <= 16384) {
-            a32.assign(a16.begin(), a16.end());
-            he = hipMalloc(reinterpret_cast<void **>(&ctx->adj32), rows * 4);
-            if (he == hipSuccess)
-                he = hipMemcpyAsync(ctx->adj32, a32.data(), rows * 4, hipMemcpyHostToDevice,
-                                    ctx->stream);
-        }
         if (he == hipSuccess && maxin <= SDNR_WAVE) {
             he = hipMalloc(reinterpret_cast<void **>(&ctx->deg32), d32.size() * 4);
             if (he == hipSuccess)

@@ -58,8 +58,6 @@ struct sdnr_ctx {
     uint16_t *adj16 = nullptr;          // (V+1) rows x 64 u16, sentinel V (V < 65535)
     uint16_t *radj16 = nullptr;         // in-neighbour rows, same layout (== adj16 if symmetric)
     uint32_t *deg32 = nullptr;          // out-degrees of 0..V (sentinel V: 0)
-    int32_t *adj32 = nullptr;           // adj16 widened to int32 (V <= 16384): rows the
-                                        // search wave prefetches land without a mask op
     bool radj_owned = false;
 
     // grow-only device scratch / staging

@@ -1070,9 +1070,13 @@ __device__ __forceinline__ int split_row(const void *__restrict__ rows,
     return x < V ? x : -1;                     // padding (-1, 0xFFFF, 0x1FFFF)
 }
 
+// visited-bit word w lives at w ^ ((w >> 5) & 31): words 32 apart (ids 1,024
+// apart -- a 32^3 torus's z neighbours) fall in different LDS banks
+__device__ __forceinline__ int vsw(int w) { return w ^ ((w >> 5) & 31); }
+
 __host__ __device__ inline size_t split_lds_words(int V, int ring, int ns, bool hops)
 {
-    const size_t VWp = (size_t)((((V + 31) >> 5) + 3) & ~3);
+    const size_t VWp = (size_t)((((V + 31) >> 5) + 31) & ~31);
     return (size_t)ns * (VWp + 2 * (size_t)ring) + (size_t)ns * kSplitQ * (hops ? 3 : 2) +
            ((3 * (size_t)ns + 3) & ~(size_t)3);
 }
@@ -1091,7 +1095,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
     static_assert(K <= 64, "one stack slot per lane");
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int VW = (V + 31) >> 5;
-    const int VWp = (VW + 3) & ~3;
+    const int VWp = (VW + 31) & ~31;          // whole 32-word blocks (swizzled)
     const int per = VWp + 2 * RING;           // words per search wave: vis | stack ring
     uint2 *qrec = reinterpret_cast<uint2 *>(lds + NS * per);
     uint32_t *qdep = reinterpret_cast<uint32_t *>(qrec + NS * kSplitQ);
@@ -1129,9 +1133,9 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                 }
                 continue;
             }
-            for (int i = lane; i < VW; i += SDNR_WAVE) vis[i] = 0u;
+            for (int i = lane; i < VWp; i += SDNR_WAVE) vis[i] = 0u;
             if (lane == 0) {                       // the wave's LDS ops stay in order
-                vis[s >> 5] = 1u << (s & 31);
+                vis[vsw(s >> 5)] = 1u << (s & 31);
                 prow[s] = PACKED ? (int32_t)((uint32_t)s | 0xFFFF0000u) : s;
                 if (!PACKED) trow[s] = -1;
                 if (HOPS) hrow[s] = 0;
@@ -1140,6 +1144,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             int lsp = 1, bot = 0, gsp = 0;
+            int pubd = pub;                        // records announced to the writer
             for (;;) {
                 if (lsp == 0) {
                     if (gsp == 0) break;
@@ -1152,16 +1157,27 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                     lsp = n;
                 }
                 const int kk = lsp < K ? lsp : K;
-                uint2 me = ring[(bot + lsp - 1 - lane) & (RING - 1)];
-                me.x = lane < kk ? me.x : 0u;
-                me.y = lane < kk ? me.y : 0u;
+                // every lane reads its slot's stack entry itself (no
+                // cross-lane shuffle on the chain); slots past the stack
+                // become vertex 0 and are masked below
+                // (one slot per lane group: J == 1; with several groups per
+                // lane, one read per lane + shuffles moves fewer LDS bytes)
+                uint2 ue[J];
                 int x[J];
+                if (J == 1) {
+                    ue[0] = ring[(bot + lsp - 1 - sub) & (RING - 1)];
+                    ue[0].x = sub < kk ? ue[0].x : 0u;
+                } else {
+                    uint2 me = ring[(bot + lsp - 1 - lane) & (RING - 1)];
+                    me.x = lane < kk ? me.x : 0u;
 #pragma unroll
-                for (int j = 0; j < J; ++j) {
-                    const int slot = j * R + sub;
-                    const int u = __shfl((int)me.x, slot);           // slot >= kk: vertex 0
-                    x[j] = split_row<FMT>(rows, rhi, V, W, u, pos);
+                    for (int j = 0; j < J; ++j) {
+                        ue[j].x = (uint32_t)__shfl((int)me.x, j * R + sub);
+                        ue[j].y = (uint32_t)__shfl((int)me.y, j * R + sub);
+                    }
                 }
+#pragma unroll
+                for (int j = 0; j < J; ++j) x[j] = split_row<FMT>(rows, rhi, V, W, (int)ue[j].x, pos);
 #pragma unroll
                 for (int j = 0; j < J; ++j) {
                     const int ok = -(int)(((j * R + sub) < kk) & (pos < W));
@@ -1171,8 +1187,17 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
 #pragma unroll
                 for (int j = 0; j < J; ++j) {
                     const int xi = x[j] & 0x7FFFFFFF;
-                    const uint32_t wv = vis[(xi >> 5) & ((x[j] >> 31) ^ -1)];
+                    const uint32_t wv = vis[vsw((xi >> 5) & ((x[j] >> 31) ^ -1))];
                     m[j] = __ballot((x[j] >= 0) & (((wv >> (xi & 31)) & 1u) == 0u));
+                }
+                // announce the previous push's records now: the LDS reads of
+                // this batch have already waited for those writes, so the
+                // LDS-only release costs no extra round trip
+                if (pub != pubd) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                    if (lane == 0) __hip_atomic_store(&ctl[w], pub, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                    pubd = pub;
                 }
                 int jstar = J;
 #pragma unroll
@@ -1184,29 +1209,39 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                 }
                 uint64_t mj = 0;
                 int vv = -1;
+                uint2 uj = make_uint2(0u, 0u);
 #pragma unroll
                 for (int j = 0; j < J; ++j)
                     if (j == jstar) {
                         mj = m[j];
                         vv = x[j];
+                        uj = ue[j];
                     }
                 const int sstar = (__ffsll((unsigned long long)mj) - 1) / LPR;
                 const int istar = jstar * R + sstar;
                 const uint64_t mm = mj & (lowmask << (sstar * LPR));
-                const int eu = read_lane((int)me.x, istar);
-                const uint32_t ed = (uint32_t)read_lane((int)me.y, istar);
+                const int eu = read_lane((int)uj.x, sstar * LPR);
+                const uint32_t ed = (uint32_t)read_lane((int)uj.y, sstar * LPR);
                 lsp -= istar + 1;
                 const int cnt = __popcll(mm);
                 // room in the record queue (the writer publishes its progress)
-                for (unsigned spin = 0; pub + cnt - cons > kSplitQ; ++spin) {
-                    cons = __hip_atomic_load(&ctl[NS + w], __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (pub + cnt - cons <= kSplitQ) break;
-                    if (spin > kSpin) {
-                        if (lane == 0) atomicOr(err, 4);
-                        break;
+                if (pub + cnt - cons > kSplitQ) {
+                    if (pub != pubd) {             // the writer must see what is queued
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                        if (lane == 0) __hip_atomic_store(&ctl[w], pub, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+                        pubd = pub;
                     }
-                    __builtin_amdgcn_s_sleep(1);
+                    for (unsigned spin = 0; pub + cnt - cons > kSplitQ; ++spin) {
+                        cons = __hip_atomic_load(&ctl[NS + w], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (pub + cnt - cons <= kSplitQ) break;
+                        if (spin > kSpin) {
+                            if (lane == 0) atomicOr(err, 4);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
                 }
                 if (lsp + cnt > RING) {            // spill the oldest half
                     for (int i = lane; i < RING / 2; i += SDNR_WAVE)
@@ -1217,7 +1252,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                 }
                 if ((mm >> lane) & 1ull) {
                     const int rank = lanes_below(mm);
-                    atomicOr(&vis[vv >> 5], 1u << (vv & 31));
+                    atomicOr(&vis[vsw(vv >> 5)], 1u << (vv & 31));
                     q[(pub + rank) & (kSplitQ - 1)] =
                         make_uint2((uint32_t)vv | ((uint32_t)pos << 26), (uint32_t)eu);
                     if (HOPS) qd[(pub + rank) & (kSplitQ - 1)] = ed + 1u;
@@ -1225,6 +1260,8 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                 }
                 lsp += cnt;
                 pub += cnt;
+            }
+            if (pub != pubd) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
                 if (lane == 0) __hip_atomic_store(&ctl[w], pub, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1242,7 +1279,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                 __builtin_amdgcn_s_sleep(1);
             }
             for (int v = lane; v < V; v += SDNR_WAVE) {
-                if (((vis[v >> 5] >> (v & 31)) & 1u) == 0u) {
+                if (((vis[vsw(v >> 5)] >> (v & 31)) & 1u) == 0u) {
                     prow[v] = -1;
                     if (!PACKED) trow[v] = -1;
                     if (HOPS) hrow[v] = -1;
@@ -1335,19 +1372,9 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int swz(int x) { return lds_swz(x); }   // common.h
 
-// lane's entry of u's 64-wide row, int32: a prefetched row can sit in its
-// register across the loop back-edge (a u16 row needs a zero-extension mask,
-// which the compiler places at the back-edge -- where it waits for the
-// prefetch to land and serialises the search again)
-template <typename AT>
-__device__ __forceinline__ int adjrow(const AT *__restrict__ adj, int u, int lane)
-{
-    return (int)adj[(size_t)u * 64 + lane];
-}
-
-template <int NW, bool HOPS, bool PACKED, typename AT = int32_t>
+template <int NW, bool HOPS, bool PACKED>
 __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
-    int V, const AT *__restrict__ adj, const uint16_t *__restrict__ radj,
+    int V, const uint16_t *__restrict__ adj, const uint16_t *__restrict__ radj,
     const uint32_t *__restrict__ deg, const int32_t *__restrict__ row_ptr,
     const int32_t *__restrict__ port, int W, const int32_t *__restrict__ ell_port,
     const int32_t *__restrict__ src, int nsrc, int32_t *__restrict__ out_parent,
@@ -1433,85 +1460,60 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             int pub = 1, pubd = 1, sp = 1, lo = 0;       // published / announced
             int pu0 = -1, pu1 = -1, xpre0 = V, xpre1 = V;   // rows of the two largest children
 #ifdef SDNR_STAMPS
-            unsigned long long st_t0, st_t1, st_cand = 0, st_false = 0, st_bp = 0, st_miss = 0,
-                                               st_skip = 0, st_find = 0, st_row = 0, st_push = 0,
-                                               st_a, st_b, st_c;
+            unsigned long long st_t0, st_t1, st_row = 0, st_cand = 0, st_false = 0, st_bp = 0,
+                                               st_miss = 0, st_skip = 0, st_tc = 0, st_skipc = 0,
+                                               st_pushc = 0;
             SDNR_STAMP(st_t0);
-            st_c = st_t0;
+            st_tc = st_t0;
 #endif
-            // children of the last push: their lanes of the row (kx), the
-            // fresh mask (km) and their counts (kc, gathered at the push,
-            // consumed one iteration later so the LDS round trip overlaps
-            // the row prefetch)
-            uint64_t km = 0;
-            int kx = V;
-            uint32_t kc = 0;
             for (;;) {
-                int u = -1;
-                if (km) {
-                    // the next pop is one of these children whenever one of
-                    // them has a non-zero count: they are the top of the
-                    // stack, highest lane (largest id, pushed last) on top,
-                    // and every child above the first live one is a leaf pop
-                    const uint64_t live = __ballot(kc != 0u) & km;
-                    if (live) {
-                        const int top = highest_lane(live);
-                        u = read_lane(kx, top);
-                        const uint64_t above = top == 63 ? 0ull : km & (~0ull << (top + 1));
-                        sp -= __popcll(above) + 1;
-                    } else {
-                        sp -= __popcll(km);       // all of them leaf pops
-                    }
-                    km = 0;
-                }
-                if (u < 0) {
-                    uint64_t m = 0;
-                    int e = V;
-                    while (sp > 0) {
+                uint64_t m = 0;
+                int e = V;
+                while (sp > 0) {
 #ifdef SDNR_STAMPS
-                        st_skip++;
+                    st_skip++;
 #endif
-                        const int kk = sp < 64 ? sp : 64;
-                        const int at = sp - 1 - lane;
-                        e = stk[at < 0 ? 0 : at];
-                        e = lane < kk ? e : V;
-                        const uint32_t c = __hip_atomic_load(&cnt[swz(e)], __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_WORKGROUP);
-                        m = __ballot(c != 0u);
-                        if (m) break;
-                        sp -= kk;
-                    }
-                    if (m) {
-                        const int first = __ffsll((unsigned long long)m) - 1;
-                        u = read_lane(e, first);
-                        sp -= first + 1;
-                    }
+                    const int kk = sp < 64 ? sp : 64;
+                    const int at = sp - 1 - lane;
+                    e = stk[at < 0 ? 0 : at];
+                    e = lane < kk ? e : V;
+                    const uint32_t c = __hip_atomic_load(&cnt[swz(e)], __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+                    m = __ballot(c != 0u);
+                    if (m) break;
+                    sp -= kk;
                 }
-                // publish the previous push's children: LDS-only release (the
-                // ring lives in LDS; a full fence would also wait for the row
-                // prefetches still in flight)
+                // publish the previous push's children now: the skip's LDS
+                // reads have waited for those writes, so the release is free
                 if (pub != pubd) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                     if (lane == 0) __hip_atomic_store(&ctl[0], pub, __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_WORKGROUP);
                     pubd = pub;
                 }
-                if (u < 0) break;
+                if (!m) break;
+                const int first = __ffsll((unsigned long long)m) - 1;
+                const int u = read_lane(e, first);
+                sp -= first + 1;
 #ifdef SDNR_STAMPS
+                unsigned long long ta, tb;
+                SDNR_STAMP(ta);
+                st_skipc += ta - st_tc;
                 if (u != pu0 && u != pu1) st_miss++;
-                st_cand++;
-                SDNR_STAMP(st_a);
-                st_find += st_a - st_c;
 #endif
-                const int x = (u == pu0) ? xpre0 : (u == pu1) ? xpre1 : adjrow(adj, u, lane);
+                const int x = (u == pu0) ? xpre0 : (u == pu1) ? xpre1
+                                                              : (int)adj[(size_t)u * 64 + lane];
                 const uint32_t wv = vis[x >> 5];
                 const bool fresh = ((wv >> (x & 31)) & 1u) == 0u;
                 const uint64_t mm = __ballot(fresh);
 #ifdef SDNR_STAMPS
+                SDNR_STAMP(tb);
+                st_row += tb - ta;
+                st_cand++;
                 if (mm == 0) st_false++;
-                SDNR_STAMP(st_b);
-                st_row += st_b - st_a;
-                st_c = st_b;
+#endif
+#ifdef SDNR_STAMPS
+                if (mm == 0) st_tc = tb;
 #endif
                 if (mm == 0) continue;           // stale count: a leaf pop after all
                 const int c = __popcll(mm);
@@ -1520,13 +1522,8 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                 pu0 = read_lane(x, highest_lane(mm));
                 const uint64_t rest = mm & ~(1ull << highest_lane(mm));
                 pu1 = rest ? read_lane(x, highest_lane(rest)) : -1;
-                xpre0 = adjrow(adj, pu0, lane);
-                xpre1 = adjrow(adj, rest ? pu1 : V, lane);
-                // the children's counts, for the next iteration
-                kc = fresh ? __hip_atomic_load(&cnt[swz(x)], __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP) : 0u;
-                km = mm;
-                kx = x;
+                xpre0 = adj[(size_t)pu0 * 64 + lane];
+                xpre1 = adj[(size_t)(rest ? pu1 : V) * 64 + lane];
                 int du = 0;
                 if (HOPS) du = uniform((int)dep[u]);
                 // back-pressure: ring slots below every worker's progress are
@@ -1557,8 +1554,8 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                 pub += c;
                 sp += c;
 #ifdef SDNR_STAMPS
-                SDNR_STAMP(st_c);
-                st_push += st_c - st_b;
+                SDNR_STAMP(st_tc);
+                st_pushc += st_tc - tb;
 #endif
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1567,13 +1564,13 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             SDNR_STAMP(st_t1);
             if (lane == 0) {
                 atomicAdd(&g_stamp[0], st_t1 - st_t0);   // search wave lifetime
-                atomicAdd(&g_stamp[1], st_row);          // candidate -> row + visited ballot
+                atomicAdd(&g_stamp[1], st_row);          // row + gather cycles
                 atomicAdd(&g_stamp[2], st_cand);         // candidates popped
                 atomicAdd(&g_stamp[3], st_false);        // ... with no fresh child
                 atomicAdd(&g_stamp[4], st_bp);           // back-pressure sleeps
                 atomicAdd(&g_stamp[5], st_skip * 1000000ull + st_miss);   // skips, prefetch misses
-                atomicAdd(&g_stamp[6], st_find);         // loop top -> candidate found
-                atomicAdd(&g_stamp[7], st_push);         // push (non-false candidates)
+                atomicAdd(&g_stamp[6], st_skipc);        // skip cycles
+                atomicAdd(&g_stamp[7], st_pushc);        // push+publish cycles
             }
 #endif
         } else {
@@ -2024,8 +2021,7 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
     const char *force = getenv("SDNROUTE_DFS_STRATEGY");
     const bool count_ok = ctx->adj16 != nullptr && ctx->radj16 != nullptr && V < 65535 &&
                           dfs_lds_bytes_count(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;
-    const bool async_ok = count_ok && ctx->adj32 != nullptr &&
-                          dfs_lds_bytes_async(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;
+    const bool async_ok = count_ok && dfs_lds_bytes_async(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;
     const bool async = async_ok && (force ? !strcmp(force, "async") : small);
     if (!async && !small && ell && ctx->W <= 32 && packed_ok() && split_ok() &&
         (!packed || (ctx->ell16 && V <= 65535)))
@@ -2064,31 +2060,14 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
     do {                                                                                     \
         auto k = dfs_async_kernel<N_, H_, P_>;                                               \
         allow_full_lds(k);                                                                   \
-        hipLaunchKernelGGL(k, dim3(cgrid), dim3(N_ * 64), cl, ctx->stream, V, ctx->adj32,    \
+        hipLaunchKernelGGL(k, dim3(cgrid), dim3(N_ * 64), cl, ctx->stream, V, ctx->adj16,    \
                            ctx->radj16, ctx->deg32, ctx->row_ptr, ctx->port, ctx->W,         \
                            ctx->ell_port, d_src, nsrc,                                       \
                            P_ ? reinterpret_cast<int32_t *>(d_tree) : d_parent, d_port,      \
                            d_hops, err);                                                     \
     } while (0)
 #define SDNR_ASYNC(N_, H_) SDNR_ASYNC_P(N_, H_, false)
-        const char *r16 = getenv("SDNROUTE_DFS_ROW16");      // A/B: u16 search rows
-        if (r16 && !strcmp(r16, "1") && nw == 4) {
-            ctx->last_kernel = packed ? "dfs_async_kernel<4,packed,row16>" : "dfs_async_kernel<4,row16>";
-#define SDNR_ASYNC16(H_, P_)                                                                 \
-    do {                                                                                     \
-        auto k = dfs_async_kernel<4, H_, P_, uint16_t>;                                      \
-        allow_full_lds(k);                                                                   \
-        hipLaunchKernelGGL(k, dim3(cgrid), dim3(4 * 64), cl, ctx->stream, V, ctx->adj16,     \
-                           ctx->radj16, ctx->deg32, ctx->row_ptr, ctx->port, ctx->W,         \
-                           ctx->ell_port, d_src, nsrc,                                       \
-                           P_ ? reinterpret_cast<int32_t *>(d_tree) : d_parent, d_port,      \
-                           d_hops, err);                                                     \
-    } while (0)
-            if (packed) SDNR_ASYNC16(false, true);
-            else if (hops) SDNR_ASYNC16(true, false);
-            else SDNR_ASYNC16(false, false);
-#undef SDNR_ASYNC16
-        } else if (packed) {
+        if (packed) {
             static const char *pnames[] = {"", "", "dfs_async_kernel<2,packed>",
                                            "dfs_async_kernel<3,packed>",
                                            "dfs_async_kernel<4,packed>",

@@ -649,6 +649,139 @@ __global__ __launch_bounds__(NW * 64) void bfs_dest_lanes_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Bit-plane multi-destination BFS with fused next hops (large V: Jellyfish
+// 100k, where neither per-destination kernel's LDS state fits).
+//
+// msbfs_level_kernel + nexthop_kernel spend most of their time in the next
+// hop pass: every (destination, vertex) gathers the distances of its W
+// neighbours again (1.6e11 gathers for all Jellyfish pairs).  The pull step
+// already has what it needs: x joins level L+1 of destination b through the
+// first (smallest id = smallest slot, the reference's lexicographic
+// tie-break) out-neighbour whose level-L frontier word holds bit b.  So the
+// level kernel, walking x's ELL row in slot order, assigns each newly
+// reached bit the slot that first supplied it and accumulates, per (batch,
+// vertex), bit-sliced planes: 8 planes of the level (L < 256) and
+// ceil(log2 W) planes of the slot, next to the visited / frontier words.
+// The tables are then written once, coalesced, by a pass that decodes the
+// planes for the 64 destinations of a word (dist, nh = row[slot],
+// nh_port = port row[slot]).  Destinations run in chunks of 64-destination
+// batches so the scratch stays bounded.
+// ---------------------------------------------------------------------------
+constexpr int kPlVis = 0, kPlFront = 1, kPlNext = 2, kPlDist = 3, kPlSlot = 11;
+constexpr int kPlanes = 16;                    // vis, front, next, 8 level, 5 slot
+
+__global__ __launch_bounds__(256) void msbfs_plane_seed_kernel(
+    int V, const int32_t *__restrict__ dst, int ndst, uint64_t *__restrict__ pl)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ndst) return;
+    const int d = dst[i];
+    if (d < 0 || d >= V) return;
+    uint64_t *b = pl + (size_t)(i >> 6) * kPlanes * V;
+    atomicOr((unsigned long long *)&b[(size_t)kPlVis * V + d], 1ull << (i & 63));
+    atomicOr((unsigned long long *)&b[(size_t)kPlFront * V + d], 1ull << (i & 63));
+}
+
+template <int SB>
+__global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
+    int V, int W, const int32_t *__restrict__ ell_col, int ndst, int lvl, int flip,
+    uint64_t *__restrict__ pl, int *__restrict__ changed)
+{
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int batch = blockIdx.y;
+    if (x >= V) return;
+    uint64_t *b = pl + (size_t)batch * kPlanes * V;
+    const uint64_t *front = b + (size_t)(flip ? kPlNext : kPlFront) * V;
+    uint64_t *next = b + (size_t)(flip ? kPlFront : kPlNext) * V;
+    const int nb = min(64, ndst - batch * 64);
+    const uint64_t all = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
+    const uint64_t vx = b[(size_t)kPlVis * V + x];
+    if ((vx & all) == all) {                   // every destination reached x already
+        next[x] = 0ull;
+        return;
+    }
+    // slot order = ascending neighbour id: a bit takes the first slot whose
+    // frontier word has it; W independent loads in flight
+    constexpr int WM = 1 << SB;                // row slots this instance handles
+    const int32_t *r = ell_col + (size_t)x * W;
+    uint64_t f[WM];
+#pragma unroll
+    for (int j = 0; j < WM; ++j) {
+        if (j < W) {
+            const int n = r[j];
+            f[j] = n >= 0 ? front[n] : 0ull;
+        }
+    }
+    uint64_t rem = ~vx & all, sp[SB];
+#pragma unroll
+    for (int k = 0; k < SB; ++k) sp[k] = 0ull;
+#pragma unroll
+    for (int j = 0; j < WM; ++j) {
+        if (j < W) {
+            const uint64_t h = f[j] & rem;
+            rem &= ~h;
+#pragma unroll
+            for (int k = 0; k < SB; ++k)
+                if ((j >> k) & 1) sp[k] |= h;
+        }
+    }
+    const uint64_t nw = (~vx & all) & ~rem;    // bits reached at this level
+    next[x] = nw;
+    if (nw) {
+        b[(size_t)kPlVis * V + x] = vx | nw;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if ((lvl >> k) & 1) b[(size_t)(kPlDist + k) * V + x] |= nw;
+#pragma unroll
+        for (int k = 0; k < SB; ++k)
+            if (sp[k]) b[(size_t)(kPlSlot + k) * V + x] |= sp[k];
+        *changed = 1;
+    }
+}
+
+// decode the planes of one batch into 64 table rows, coalesced along x
+template <int SB>
+__global__ __launch_bounds__(256) void msbfs_plane_tables_kernel(
+    int V, int W, const int32_t *__restrict__ ell_col, const int32_t *__restrict__ ell_port,
+    int ndst, const uint64_t *__restrict__ pl, uint16_t *__restrict__ dist,
+    int32_t *__restrict__ nh, int32_t *__restrict__ nh_port)
+{
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int batch = blockIdx.y;
+    if (x >= V) return;
+    const uint64_t *b = pl + (size_t)batch * kPlanes * V;
+    const uint64_t vx = b[(size_t)kPlVis * V + x];
+    uint64_t d[8], s[SB];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = b[(size_t)(kPlDist + k) * V + x];
+#pragma unroll
+    for (int k = 0; k < SB; ++k) s[k] = b[(size_t)(kPlSlot + k) * V + x];
+    const int nb = min(64, ndst - batch * 64);
+    for (int i = 0; i < nb; ++i) {
+        const size_t row = (size_t)(batch * 64 + i) * V + x;
+        uint32_t L = 0xFFFFu;
+        int best = -1, bport = -1;
+        if ((vx >> i) & 1ull) {
+            L = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) L |= (uint32_t)((d[k] >> i) & 1ull) << k;
+            if (L) {
+                int sl = 0;
+#pragma unroll
+                for (int k = 0; k < SB; ++k) sl |= (int)((s[k] >> i) & 1ull) << k;
+                best = ell_col[(size_t)x * W + sl];
+                if (nh_port) bport = ell_port[(size_t)x * W + sl];
+            }
+        }
+        dist[row] = (uint16_t)L;
+        if (nh) {
+            nh[row] = best;
+            nh_port[row] = bport;
+        }
+    }
+}
+
 }  // namespace
 
 // SDNROUTE_SP_STRATEGY=msbfs|lanes forces the shortest-mode kernel (tests)
@@ -656,6 +789,69 @@ static const char *sp_strategy()
 {
     const char *f = getenv("SDNROUTE_SP_STRATEGY");
     return f ? f : "";
+}
+
+// bit-plane BFS (msbfs_plane_*): returns 1 (nothing launched that matters,
+// tables to be redone) if a BFS is deeper than the 255 levels the planes hold
+static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint16_t *d_dist,
+                        int32_t *d_nh, int32_t *d_nh_port)
+{
+    const int V = ctx->V, W = ctx->W;
+    const int sb = W <= 16 ? 4 : 5;
+    const int nbatch = (ndst + 63) / 64;
+    const size_t per_batch = (size_t)kPlanes * V * sizeof(uint64_t);
+    int cb = (int)((size_t)(4ull << 30) / per_batch);   // <= 4 GiB of planes at a time
+    if (cb < 1) cb = 1;
+    if (cb > nbatch) cb = nbatch;
+    int rc = sdnr_reserve(&ctx->scratch, &ctx->scratch_bytes, (size_t)cb * per_batch + 256);
+    if (rc) return rc;
+    uint64_t *pl = static_cast<uint64_t *>(ctx->scratch);
+    int *changed = reinterpret_cast<int *>(reinterpret_cast<char *>(ctx->scratch) +
+                                           (size_t)cb * per_batch);
+    const int gx = (V + 255) / 256;
+    int levels = 0;
+    for (int c0 = 0; c0 < nbatch; c0 += cb) {
+        const int nbc = nbatch - c0 < cb ? nbatch - c0 : cb;
+        const int nd = ndst - c0 * 64 < nbc * 64 ? ndst - c0 * 64 : nbc * 64;
+        SDNR_HIP(hipMemsetAsync(pl, 0, (size_t)nbc * per_batch, ctx->stream));
+        hipLaunchKernelGGL(msbfs_plane_seed_kernel, dim3((nd + 255) / 256), dim3(256), 0,
+                           ctx->stream, V, d_dst + (size_t)c0 * 64, nd, pl);
+        SDNR_HIP(hipGetLastError());
+        int h_changed = 1, lvl = 1;
+        for (; lvl < 256 && h_changed; ++lvl) {
+            SDNR_HIP(hipMemsetAsync(changed, 0, sizeof(int), ctx->stream));
+            if (sb == 4)
+                hipLaunchKernelGGL(msbfs_plane_level_kernel<4>, dim3(gx, nbc), dim3(256), 0,
+                                   ctx->stream, V, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
+                                   changed);
+            else
+                hipLaunchKernelGGL(msbfs_plane_level_kernel<5>, dim3(gx, nbc), dim3(256), 0,
+                                   ctx->stream, V, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
+                                   changed);
+            SDNR_HIP(hipGetLastError());
+            SDNR_HIP(hipMemcpyAsync(&h_changed, changed, sizeof(int), hipMemcpyDeviceToHost,
+                                    ctx->stream));
+            SDNR_HIP(hipStreamSynchronize(ctx->stream));
+        }
+        if (h_changed) return 1;                 // deeper than 255 levels
+        levels += lvl - 1;
+        uint16_t *dist = d_dist + (size_t)c0 * 64 * V;
+        int32_t *nh = d_nh ? d_nh + (size_t)c0 * 64 * V : nullptr;
+        int32_t *nhp = d_nh_port ? d_nh_port + (size_t)c0 * 64 * V : nullptr;
+        if (sb == 4)
+            hipLaunchKernelGGL(msbfs_plane_tables_kernel<4>, dim3(gx, nbc), dim3(256), 0,
+                               ctx->stream, V, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
+                               nhp);
+        else
+            hipLaunchKernelGGL(msbfs_plane_tables_kernel<5>, dim3(gx, nbc), dim3(256), 0,
+                               ctx->stream, V, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
+                               nhp);
+        SDNR_HIP(hipGetLastError());
+    }
+    ctx->last_launches = levels;
+    ctx->last_kernel = "msbfs_plane_level_kernel+msbfs_plane_tables_kernel";
+    if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+    return SDNR_OK;
 }
 
 int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
@@ -669,7 +865,12 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
     const bool dest_ok = ctx->adj16 != nullptr && ctx->radj16 != nullptr && V < 65534 &&
                          dlds <= 64 * 1024;
     const char *force = sp_strategy();
-    if (dest_ok && strcmp(force, "msbfs") != 0 && strcmp(force, "lanes") != 0) {
+    if (!strcmp(force, "plane") && ctx->W > 0 && ctx->W <= 32) {
+        const int rc = launch_plane(ctx, d_dst, ndst, d_dist, d_nh, d_nh_port);
+        if (rc <= 0) return rc;
+    }
+    if (dest_ok && strcmp(force, "msbfs") != 0 && strcmp(force, "lanes") != 0 &&
+        strcmp(force, "plane") != 0) {
         const bool sym = ctx->radj16 == ctx->adj16;
         size_t bpc = SDNR_LDS_PER_CU / dlds;
         if (bpc > 8) bpc = 8;
@@ -711,7 +912,7 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
     const size_t llds = bfs_lanes_bytes(V, lpr);
     const bool lanes_ok = ctx->adj16 != nullptr && ctx->radj16 != nullptr && V < 65534 &&
                           maxrow <= 32 && llds <= SDNR_MAX_LDS_PER_BLOCK - 1024;
-    if (lanes_ok && strcmp(force, "msbfs") != 0) {
+    if (lanes_ok && strcmp(force, "msbfs") != 0 && strcmp(force, "plane") != 0) {
         const bool sym = ctx->radj16 == ctx->adj16;
         size_t bpc = SDNR_LDS_PER_CU / llds;
         if (bpc > 2) bpc = 2;
@@ -760,8 +961,14 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
         if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
         return SDNR_OK;
     }
-    SDNR_HIP(hipMemsetAsync(d_dist, 0xFF, (size_t)ndst * V * sizeof(uint16_t), ctx->stream));
     const size_t lds = (size_t)V * 3 * sizeof(uint64_t);
+    // large graphs with ELL rows: the bit-plane BFS with fused next hops
+    // (SDNROUTE_SP_STRATEGY=msbfs keeps the level + next-hop pair)
+    if (lds > 150 * 1024 && ctx->W > 0 && ctx->W <= 32 && strcmp(force, "msbfs") != 0) {
+        const int rc = launch_plane(ctx, d_dst, ndst, d_dist, d_nh, d_nh_port);
+        if (rc <= 0) return rc;                  // else: too deep, redo below
+    }
+    SDNR_HIP(hipMemsetAsync(d_dist, 0xFF, (size_t)ndst * V * sizeof(uint16_t), ctx->stream));
     ctx->last_kernel = lds <= 150 * 1024 ? "msbfs_lds_kernel+nexthop_kernel"
                                          : "msbfs_level_kernel+nexthop_kernel";
     if (lds <= 150 * 1024) {

@@ -199,7 +199,7 @@ def test_dfs_fullsize_tree_properties(ctx):
             assert k < hi and csr.col[k] == v and csr.port[k] == t[s, v]
 
 
-@pytest.mark.parametrize("strategy", ["auto", "msbfs", "lanes", "lanes-csr"])
+@pytest.mark.parametrize("strategy", ["auto", "msbfs", "lanes", "lanes-csr", "plane"])
 @pytest.mark.parametrize("name", G.SMALL)
 def test_shortest_small_all_destinations(ctx, monkeypatch, name, strategy):
     if strategy == "lanes-csr":                  # no ELL copy: 64-wide rows + CSR ports
@@ -256,7 +256,7 @@ def test_shortest_fullsize_fat_tree(ctx, monkeypatch, strategy):
     np.testing.assert_array_equal(nhp, nhpo)
 
 
-@pytest.mark.parametrize("strategy", ["auto", "msbfs"])
+@pytest.mark.parametrize("strategy", ["auto", "msbfs", "plane"])
 def test_shortest_fullsize_torus_sample(ctx, monkeypatch, strategy):
     """torus 32^3 (the BASELINE multi-source BFS config), spread destinations:
     the lane-packed per-destination BFS and the 64-destination bitset BFS."""
@@ -267,8 +267,9 @@ def test_shortest_fullsize_torus_sample(ctx, monkeypatch, strategy):
     dsts = np.linspace(0, csr.V - 1, 96).astype(np.int32)
     ctx.upload(csr)
     dist, nh, nhp = ctx.shortest_tables(dsts)
-    assert ctx.last_kernel().startswith(
-        "bfs_dest_lanes_kernel<8,sym>" if strategy == "auto" else "msbfs_level_kernel")
+    assert ctx.last_kernel().startswith({"auto": "bfs_dest_lanes_kernel<8,sym>",
+                                         "msbfs": "msbfs_level_kernel",
+                                         "plane": "msbfs_plane_level_kernel"}[strategy])
     do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
     np.testing.assert_array_equal(dist, do)
     np.testing.assert_array_equal(nh, nho)
@@ -524,24 +525,17 @@ def test_ecmp_counts_vs_level_dp(ctx, case):
         assert int(paths[0, csr.V - 1]) == 2**64 - 1
 
 
-@pytest.mark.parametrize("packed", [True, False])
-@pytest.mark.parametrize("name", ["fat_tree_k8", "jellyfish_n60_r5", "torus_5x3x2", "random_V40",
-                                  "dragonfly_a4_h2_p2"])
-def test_dfs_async_row16(ctx, monkeypatch, name, packed):
-    """The async kernel with u16 search rows (A/B variant of the int32 rows)."""
-    _strategy(monkeypatch, "async")
-    monkeypatch.setenv("SDNROUTE_DFS_ROW16", "1")
-    csr = G.Golden(name).fabric().csr()
-    srcs = np.arange(csr.V, dtype=np.int32)
+
+def test_shortest_plane_too_deep_falls_back(ctx, monkeypatch):
+    """A ring of 700 switches (BFS depth 350 > the 255 levels the bit planes
+    hold): the plane path hands over to the level + next-hop kernels."""
+    monkeypatch.setenv("SDNROUTE_SP_STRATEGY", "plane")
+    csr = T.torus3d(700, 1, 1).csr()
+    dsts = np.arange(0, csr.V, 7, dtype=np.int32)
     ctx.upload(csr)
-    po, to, ho = O.dfs_tables(csr, srcs, nthreads=NTHREADS)
-    if packed:
-        tree = ctx.dfs_tables_packed(srcs)
-        assert ctx.last_kernel() == "dfs_async_kernel<4,packed,row16>"
-        np.testing.assert_array_equal(tree, _pack(po, to))
-    else:
-        p, t, h = ctx.dfs_tables(srcs)
-        assert ctx.last_kernel() == "dfs_async_kernel<4,row16>"
-        np.testing.assert_array_equal(p, po)
-        np.testing.assert_array_equal(t, to)
-        np.testing.assert_array_equal(h, ho)
+    dist, nh, nhp = ctx.shortest_tables(dsts)
+    assert not ctx.last_kernel().startswith("msbfs_plane")
+    do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
+    np.testing.assert_array_equal(dist, do)
+    np.testing.assert_array_equal(nh, nho)
+    np.testing.assert_array_equal(nhp, nhpo)
