@@ -797,7 +797,7 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
                         int32_t *d_nh, int32_t *d_nh_port)
 {
     const int V = ctx->V, W = ctx->W;
-    const int sb = W <= 16 ? 4 : 5;
+    const int sb = W <= 8 ? 3 : W <= 16 ? 4 : 5;
     const int nbatch = (ndst + 63) / 64;
     const size_t per_batch = (size_t)kPlanes * V * sizeof(uint64_t);
     int cb = (int)((size_t)(4ull << 30) / per_batch);   // <= 4 GiB of planes at a time
@@ -820,7 +820,11 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
         int h_changed = 1, lvl = 1;
         for (; lvl < 256 && h_changed; ++lvl) {
             SDNR_HIP(hipMemsetAsync(changed, 0, sizeof(int), ctx->stream));
-            if (sb == 4)
+            if (sb == 3)
+                hipLaunchKernelGGL(msbfs_plane_level_kernel<3>, dim3(gx, nbc), dim3(256), 0,
+                                   ctx->stream, V, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
+                                   changed);
+            else if (sb == 4)
                 hipLaunchKernelGGL(msbfs_plane_level_kernel<4>, dim3(gx, nbc), dim3(256), 0,
                                    ctx->stream, V, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
                                    changed);
@@ -838,7 +842,11 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
         uint16_t *dist = d_dist + (size_t)c0 * 64 * V;
         int32_t *nh = d_nh ? d_nh + (size_t)c0 * 64 * V : nullptr;
         int32_t *nhp = d_nh_port ? d_nh_port + (size_t)c0 * 64 * V : nullptr;
-        if (sb == 4)
+        if (sb == 3)
+            hipLaunchKernelGGL(msbfs_plane_tables_kernel<3>, dim3(gx, nbc), dim3(256), 0,
+                               ctx->stream, V, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
+                               nhp);
+        else if (sb == 4)
             hipLaunchKernelGGL(msbfs_plane_tables_kernel<4>, dim3(gx, nbc), dim3(256), 0,
                                ctx->stream, V, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
                                nhp);
@@ -865,7 +873,13 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
     const bool dest_ok = ctx->adj16 != nullptr && ctx->radj16 != nullptr && V < 65534 &&
                          dlds <= 64 * 1024;
     const char *force = sp_strategy();
-    if (!strcmp(force, "plane") && ctx->W > 0 && ctx->W <= 32) {
+    // the bit-plane BFS wins wherever its rows fit and the batch is not tiny
+    // (dragonfly all-pairs 0.226 -> 0.197 ms, torus 32^3 22.6 -> 16.1 ms; a
+    // 32-destination fat-tree k=8 batch is dominated by its per-level syncs);
+    // SDNROUTE_SP_STRATEGY=plane|lanes|msbfs forces a kernel family
+    const bool plane_ok = ctx->W > 0 && ctx->W <= 32;
+    const bool plane_big = (size_t)ndst * (size_t)V >= ((size_t)1 << 21);
+    if (plane_ok && (!strcmp(force, "plane") || (!*force && plane_big))) {
         const int rc = launch_plane(ctx, d_dst, ndst, d_dist, d_nh, d_nh_port);
         if (rc <= 0) return rc;
     }

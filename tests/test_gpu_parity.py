@@ -256,7 +256,7 @@ def test_shortest_fullsize_fat_tree(ctx, monkeypatch, strategy):
     np.testing.assert_array_equal(nhp, nhpo)
 
 
-@pytest.mark.parametrize("strategy", ["auto", "msbfs", "plane"])
+@pytest.mark.parametrize("strategy", ["auto", "msbfs", "plane", "lanes"])
 def test_shortest_fullsize_torus_sample(ctx, monkeypatch, strategy):
     """torus 32^3 (the BASELINE multi-source BFS config), spread destinations:
     the lane-packed per-destination BFS and the 64-destination bitset BFS."""
@@ -267,7 +267,8 @@ def test_shortest_fullsize_torus_sample(ctx, monkeypatch, strategy):
     dsts = np.linspace(0, csr.V - 1, 96).astype(np.int32)
     ctx.upload(csr)
     dist, nh, nhp = ctx.shortest_tables(dsts)
-    assert ctx.last_kernel().startswith({"auto": "bfs_dest_lanes_kernel<8,sym>",
+    assert ctx.last_kernel().startswith({"auto": "msbfs_plane_level_kernel",
+                                         "lanes": "bfs_dest_lanes_kernel<8,sym>",
                                          "msbfs": "msbfs_level_kernel",
                                          "plane": "msbfs_plane_level_kernel"}[strategy])
     do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
@@ -300,12 +301,16 @@ def test_apsp_small(ctx, monkeypatch, name, algo):
     np.testing.assert_array_equal(ctx.apsp(), O.apsp(csr))
 
 
-def test_shortest_dest_kernel_dragonfly_all_destinations(ctx):
+@pytest.mark.parametrize("strategy", ["auto", "dest"])
+def test_shortest_dest_kernel_dragonfly_all_destinations(ctx, monkeypatch, strategy):
+    if strategy == "dest":
+        monkeypatch.setenv("SDNROUTE_SP_STRATEGY", "dest")
     csr = T.dragonfly(16, 8, 8).csr()
     dsts = np.arange(csr.V, dtype=np.int32)
     ctx.upload(csr)
     dist, nh, nhp = ctx.shortest_tables(dsts)
-    assert ctx.last_kernel().startswith("bfs_dest_kernel")
+    assert ctx.last_kernel().startswith("bfs_dest_kernel" if strategy == "dest"
+                                        else "msbfs_plane_level_kernel")
     do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
     np.testing.assert_array_equal(dist, do)
     np.testing.assert_array_equal(nh, nho)
