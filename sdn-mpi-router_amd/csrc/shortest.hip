@@ -686,10 +686,14 @@ __global__ __launch_bounds__(256) void msbfs_plane_seed_kernel(
 template <int SB>
 __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
     int V, int W, const int32_t *__restrict__ ell_col, int ndst, int lvl, int flip,
-    uint64_t *__restrict__ pl, int *__restrict__ changed)
+    uint64_t *__restrict__ pl, int *changed)
 {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int batch = blockIdx.y;
+    // levels are queued ahead of the host's termination check: a level
+    // after one that reached nothing has nothing to do
+    if (lvl > 1 && __hip_atomic_load(&changed[lvl - 1], __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT) == 0) return;
     if (x >= V) return;
     uint64_t *b = pl + (size_t)batch * kPlanes * V;
     const uint64_t *front = b + (size_t)(flip ? kPlNext : kPlFront) * V;
@@ -736,7 +740,7 @@ __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
 #pragma unroll
         for (int k = 0; k < SB; ++k)
             if (sp[k]) b[(size_t)(kPlSlot + k) * V + x] |= sp[k];
-        *changed = 1;
+        changed[lvl] = 1;
     }
 }
 
@@ -801,13 +805,17 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
     const int nbatch = (ndst + 63) / 64;
     const size_t per_batch = (size_t)kPlanes * V * sizeof(uint64_t);
     int cb = (int)((size_t)(4ull << 30) / per_batch);   // <= 4 GiB of planes at a time
+    if (const char *f = getenv("SDNROUTE_PLANE_CHUNK")) {   // batches per chunk (tuning)
+        const int k = atoi(f);
+        if (k > 0) cb = k;
+    }
     if (cb < 1) cb = 1;
     if (cb > nbatch) cb = nbatch;
-    int rc = sdnr_reserve(&ctx->scratch, &ctx->scratch_bytes, (size_t)cb * per_batch + 256);
+    int rc = sdnr_reserve(&ctx->scratch, &ctx->scratch_bytes, (size_t)cb * per_batch + 1024);
     if (rc) return rc;
     uint64_t *pl = static_cast<uint64_t *>(ctx->scratch);
     int *changed = reinterpret_cast<int *>(reinterpret_cast<char *>(ctx->scratch) +
-                                           (size_t)cb * per_batch);
+                                           (size_t)cb * per_batch);   // [256] per level
     const int gx = (V + 255) / 256;
     int levels = 0;
     for (int c0 = 0; c0 < nbatch; c0 += cb) {
@@ -817,9 +825,11 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
         hipLaunchKernelGGL(msbfs_plane_seed_kernel, dim3((nd + 255) / 256), dim3(256), 0,
                            ctx->stream, V, d_dst + (size_t)c0 * 64, nd, pl);
         SDNR_HIP(hipGetLastError());
+        // levels go out in groups of kGroup with one host check per group
+        constexpr int kGroup = 8;
+        SDNR_HIP(hipMemsetAsync(changed, 0, 256 * sizeof(int), ctx->stream));
         int h_changed = 1, lvl = 1;
         for (; lvl < 256 && h_changed; ++lvl) {
-            SDNR_HIP(hipMemsetAsync(changed, 0, sizeof(int), ctx->stream));
             if (sb == 3)
                 hipLaunchKernelGGL(msbfs_plane_level_kernel<3>, dim3(gx, nbc), dim3(256), 0,
                                    ctx->stream, V, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
@@ -833,12 +843,21 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
                                    ctx->stream, V, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
                                    changed);
             SDNR_HIP(hipGetLastError());
-            SDNR_HIP(hipMemcpyAsync(&h_changed, changed, sizeof(int), hipMemcpyDeviceToHost,
-                                    ctx->stream));
-            SDNR_HIP(hipStreamSynchronize(ctx->stream));
+            if (lvl % kGroup == 0 || lvl == 255) {
+                SDNR_HIP(hipMemcpyAsync(&h_changed, changed + lvl, sizeof(int),
+                                        hipMemcpyDeviceToHost, ctx->stream));
+                SDNR_HIP(hipStreamSynchronize(ctx->stream));
+            }
         }
         if (h_changed) return 1;                 // deeper than 255 levels
-        levels += lvl - 1;
+        // levels that reached something: the queued ones after the last
+        // change returned at once
+        int hc[256];
+        SDNR_HIP(hipMemcpyAsync(hc, changed, sizeof hc, hipMemcpyDeviceToHost, ctx->stream));
+        SDNR_HIP(hipStreamSynchronize(ctx->stream));
+        lvl = 1;
+        while (lvl < 256 && hc[lvl]) ++lvl;
+        levels += lvl;
         uint16_t *dist = d_dist + (size_t)c0 * 64 * V;
         int32_t *nh = d_nh ? d_nh + (size_t)c0 * 64 * V : nullptr;
         int32_t *nhp = d_nh_port ? d_nh_port + (size_t)c0 * 64 * V : nullptr;

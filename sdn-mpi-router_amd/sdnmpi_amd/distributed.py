@@ -14,7 +14,8 @@ into an all-(-1) row; ``unpad`` drops it after the gather.
 import torch
 import torch.distributed as dist
 
-__all__ = ["shard_bounds", "padded_shard", "all_gather_rows", "all_gather_rows_async", "unpad"]
+__all__ = ["shard_bounds", "padded_shard", "all_gather_rows", "all_gather_rows_async", "unpad",
+           "sharded_route_tables"]
 
 
 def shard_bounds(n, world, rank):
@@ -82,3 +83,34 @@ class _Done(object):
 
 def unpad(table, n):
     return table[:n]
+
+
+def sharded_route_tables(db, mode="dfs", group=None):
+    """``db.route_tables(mode)`` computed by every rank of ``group`` together:
+    one process per GPU, each with its own TopologyDB over the same dicts
+    (e.g. replayed from the same Ryu events); rank r computes the rows of its
+    contiguous shard of the host-bearing switches on its own device, and one
+    all-gather per table assembles every row on every rank.  Same dict as
+    ``db.route_tables(mode)``."""
+    import numpy as np
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    ex = db.graph()
+    hv = db._host_vertices(ex)
+    lo, hi, per = shard_bounds(len(hv), world, rank)
+    t = db.route_tables(mode, vertices=hv[lo:hi])
+    names = ("parent", "port", "hops") if mode == "dfs" else ("dist", "nh", "nh_port")
+    out = dict(t)
+    for name in names:
+        a = t[name]
+        pad = np.full((per, a.shape[1]), 0xFFFF if a.dtype == np.uint16 else -1, a.dtype)
+        pad[: a.shape[0]] = a
+        loc = torch.from_numpy(pad.view(np.int16) if a.dtype == np.uint16 else pad)
+        if loc.dtype == torch.int16:                        # gloo: move the bytes
+            g = all_gather_rows(loc.view(torch.uint8)).view(torch.int16)
+        else:
+            g = all_gather_rows(loc)
+        g = unpad(g, len(hv)).numpy()
+        out[name] = g.view(np.uint16) if a.dtype == np.uint16 else g
+    out["sources" if mode == "dfs" else "destinations"] = np.asarray(hv, np.int32)
+    return out

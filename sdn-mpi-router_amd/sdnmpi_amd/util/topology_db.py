@@ -262,8 +262,10 @@ class TopologyDB(object):
                 and (in_port is None or p.port_no != in_port)]
 
     # -- batched (all-pairs) interface ---------------------------------
-    def route_tables(self, mode="dfs"):
-        """Tables for every host-bearing switch.
+    def route_tables(self, mode="dfs", vertices=None):
+        """Tables for every host-bearing switch (or the dense ``vertices``
+        given, e.g. one rank's shard: :func:`sdnmpi_amd.distributed.
+        sharded_route_tables`).
 
         ``mode="dfs"``: per-source trees of the default route,
         dict(sources, parent, port, hops, dpids);  ``mode="shortest"``:
@@ -272,7 +274,7 @@ class TopologyDB(object):
         if mode not in ("dfs", "shortest"):
             raise ValueError("mode must be 'dfs' or 'shortest'")
         ex = self.graph()
-        hv = self._host_vertices(ex)
+        hv = self._host_vertices(ex) if vertices is None else [int(v) for v in vertices]
         c = self._cache
         store = c.dfs if mode == "dfs" else c.sp
         get = c.dfs_rows if mode == "dfs" else c.sp_rows
@@ -283,7 +285,11 @@ class TopologyDB(object):
             tabs = get(self.engine, chunk)
             idx = np.asarray([store.row[v] for v in chunk], np.int64)
             parts.append(tuple(_host(_take(a, idx)) for a in tabs))
-        cols = [np.concatenate([p[k] for p in parts]) if parts else None for k in range(3)]
+        V = ex.csr.V
+        empty = (np.zeros((0, V), np.int32), np.zeros((0, V), np.int32),
+                 np.zeros((0, V), np.int32)) if mode == "dfs" else \
+            (np.zeros((0, V), np.uint16), np.zeros((0, V), np.int32), np.zeros((0, V), np.int32))
+        cols = [np.concatenate([p[k] for p in parts]) if parts else empty[k] for k in range(3)]
         if mode == "dfs":
             return {"sources": np.asarray(hv, np.int32), "parent": cols[0],
                     "port": cols[1], "hops": cols[2], "dpids": ex.csr.dpids}

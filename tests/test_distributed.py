@@ -76,3 +76,51 @@ def test_shard_bounds_cover_everything():
                 assert hi - lo <= per
                 rows += list(range(lo, hi))
             assert rows == list(range(n))
+
+
+def _db_worker(rank, world, port, fabric_name, q):
+    """Each rank: its own drop-in TopologyDB over the same topology events,
+    the oracle standing in for the GPU engine (CPU test), its shard of the
+    route tables, one all-gather per table."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "sdn-mpi-router_amd"), os.path.join(root, "tests")]
+    from test_topologydb_dropin import _FakeEngine
+    from sdnmpi_amd import distributed as D
+    from sdnmpi_amd import topologies as T
+    from sdnmpi_amd.util.topology_db import TopologyDB
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fabric = T.by_name(fabric_name)
+        db = fabric.populate(TopologyDB())
+        db._engine = _FakeEngine()
+        res = []
+        for mode in ("dfs", "shortest"):
+            got = D.sharded_route_tables(db, mode)
+            if rank == 0:
+                ref = fabric.populate(TopologyDB())
+                ref._engine = _FakeEngine()
+                want = ref.route_tables(mode)
+                res.append(all(np.array_equal(got[k], want[k]) for k in want))
+        if rank == 0:
+            q.put(all(res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fabric", [(2, "fat_tree:8"), (3, "torus:4,3,2")])
+def test_sharded_topologydb_route_tables(world, fabric):
+    """distributed.sharded_route_tables over per-rank TopologyDBs equals one
+    TopologyDB's route_tables, both modes (gloo, world size 2 and 3)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_db_worker, args=(r, world, port, fabric, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=10) is True

@@ -66,17 +66,24 @@ def main(src, out):
     return pmc
 
 
-def record_traffic(pmc, key, kernel_prefix, path):
+def record_traffic(pmc, key, kernel_prefix, path, steps=None):
     """Store the corrected HBM bytes per dispatch of the dominant kernel in
     profiles/traffic.json under `key` ("fabric/mode/N<n>"); bench.py reports
-    it as roofline.traffic."""
-    hits = [d for k, d in pmc.items() if kernel_prefix in k]
-    if not hits:
-        raise SystemExit("no PMC rows for kernel %r" % kernel_prefix)
-    c = hits[0]["counters"]
-    if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
-        raise SystemExit("FETCH_SIZE / WRITE_SIZE missing for %r" % kernel_prefix)
-    tb = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+    it as roofline.traffic.  With several "+"-separated kernel prefixes
+    (a step made of several kernels, e.g. the bit-plane BFS's level launches
+    + its table pass) and `steps` = steps the profiled run executed, the
+    value is their summed traffic per step."""
+    prefixes = kernel_prefix.split("+")
+    tb = 0.0
+    for pre in prefixes:
+        hits = [d for k, d in pmc.items() if pre in k]
+        if not hits:
+            raise SystemExit("no PMC rows for kernel %r" % pre)
+        c = hits[0]["counters"]
+        if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
+            raise SystemExit("FETCH_SIZE / WRITE_SIZE missing for %r" % pre)
+        per = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+        tb += per * (hits[0]["dispatches"] / float(steps) if len(prefixes) > 1 else 1.0)
     data = json.load(open(path)) if os.path.exists(path) else {}
     data[key] = tb
     json.dump(data, open(path, "w"), indent=1, sort_keys=True)
@@ -85,6 +92,7 @@ def record_traffic(pmc, key, kernel_prefix, path):
 
 if __name__ == "__main__":
     res = main(sys.argv[1], sys.argv[2])
-    if len(sys.argv) > 4:      # ... KEY KERNEL_PREFIX  -> profiles/traffic.json
+    if len(sys.argv) > 4:      # ... KEY KERNEL_PREFIX[+PREFIX...] [STEPS] -> profiles/traffic.json
         record_traffic(res, sys.argv[3], sys.argv[4],
-                       os.path.join(os.path.dirname(sys.argv[2]) or ".", "traffic.json"))
+                       os.path.join(os.path.dirname(sys.argv[2]) or ".", "traffic.json"),
+                       int(sys.argv[5]) if len(sys.argv) > 5 else None)
