@@ -190,6 +190,15 @@ int sdnr_route_expand(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port,
                       const int64_t *offsets, int32_t *hop_switch,
                       int32_t *hop_port, uint32_t flags);
 
+/* Flood ports (TopologyManager._is_edge_port / _do_broadcast, reference
+ * sdnmpi/topology.py:150-177): is_edge[i] = 1 iff ports[i] is neither end of
+ * any link.  Keys are (dense switch id << 32) | port_no; ends (both ends of
+ * every link, the reference's link.src and link.dst) must be sorted
+ * ascending (duplicates allowed).  Needs no uploaded graph. */
+int sdnr_edge_ports(sdnr_ctx *ctx, const uint64_t *ends, int32_t nends,
+                    const uint64_t *ports, int32_t nports, uint8_t *is_edge,
+                    uint32_t flags);
+
 /* Device time in milliseconds of the main kernel(s) of the last table call
  * made with SDNR_TIMING (waits for that call to finish). */
 int sdnr_last_kernel_ms(sdnr_ctx *ctx, float *ms);

@@ -805,6 +805,36 @@ int sdnr_ecmp_routes(sdnr_ctx *ctx, const uint16_t *dist, const uint64_t *paths,
     return SDNR_OK;
 }
 
+int sdnr_edge_ports(sdnr_ctx *ctx, const uint64_t *ends, int32_t nends, const uint64_t *ports,
+                    int32_t nports, uint8_t *is_edge, uint32_t flags)
+{
+    CHECK_CTX(ctx);
+    if (nends < 0 || nports < 0 || (nends > 0 && !ends) || (nports > 0 && (!ports || !is_edge)))
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_edge_ports: bad arguments");
+    SDNR_HIP(hipSetDevice(ctx->device));
+    ctx->timed = (flags & SDNR_TIMING) != 0;
+    ctx->last_launches = 1;
+    if (flags & SDNR_DEVICE_PTRS)
+        return sdnr_launch_edge_ports(ctx, ends, nends, ports, nports, is_edge);
+    for (int32_t i = 1; i < nends; ++i)
+        if (ends[i] < ends[i - 1])
+            return sdnr_fail(SDNR_ERR_INVAL, "sdnr_edge_ports: ends not sorted at %d", i);
+    const size_t eb = (size_t)nends * 8, pb = (size_t)nports * 8;
+    int rc = sdnr_reserve(&ctx->stage, &ctx->stage_bytes, eb + pb + (size_t)nports + 1024);
+    if (rc) return rc;
+    Stage st{static_cast<char *>(ctx->stage)};
+    uint64_t *d_e = static_cast<uint64_t *>(st.take(eb));
+    uint64_t *d_p = static_cast<uint64_t *>(st.take(pb));
+    uint8_t *d_o = static_cast<uint8_t *>(st.take((size_t)nports));
+    if (eb) SDNR_HIP(hipMemcpyAsync(d_e, ends, eb, hipMemcpyHostToDevice, ctx->stream));
+    if (pb) SDNR_HIP(hipMemcpyAsync(d_p, ports, pb, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = sdnr_launch_edge_ports(ctx, d_e, nends, d_p, nports, d_o))) return rc;
+    if (nports) SDNR_HIP(hipMemcpyAsync(is_edge, d_o, (size_t)nports, hipMemcpyDeviceToHost,
+                                        ctx->stream));
+    SDNR_HIP(hipStreamSynchronize(ctx->stream));
+    return SDNR_OK;
+}
+
 const char *sdnr_last_kernel(const sdnr_ctx *ctx) { return ctx ? ctx->last_kernel : ""; }
 
 int sdnr_last_launches(const sdnr_ctx *ctx, int32_t *launches)

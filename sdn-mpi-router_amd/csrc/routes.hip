@@ -264,6 +264,26 @@ __global__ __launch_bounds__(256) void route_walk_kernel(
     }
 }
 
+// Flood-port test of TopologyManager._is_edge_port (reference
+// sdnmpi/topology.py:150-155, used by _do_broadcast :157-177): a switch port
+// is an edge port iff it is neither end of any link.  Keys are (dense switch
+// id << 32 | port_no); the link ends arrive sorted, so each port is one
+// binary search instead of the reference's scan over every link.
+__global__ __launch_bounds__(256) void edge_port_kernel(const uint64_t *__restrict__ ends, int nends,
+                                                         const uint64_t *__restrict__ ports,
+                                                         int nports, uint8_t *__restrict__ is_edge)
+{
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nports; i += gridDim.x * blockDim.x) {
+        const uint64_t k = ports[i];
+        int lo = 0, hi = nends;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (ends[mid] < k) lo = mid + 1; else hi = mid;
+        }
+        is_edge[i] = (lo < nends && ends[lo] == k) ? 0 : 1;
+    }
+}
+
 }  // namespace
 
 int sdnr_launch_route_offsets(sdnr_ctx *ctx, const int32_t *d_hops, const int32_t *d_rows,
@@ -374,6 +394,21 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
         }
 #undef SDNR_JUMP
     }
+    SDNR_HIP(hipGetLastError());
+    if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+    return SDNR_OK;
+}
+
+int sdnr_launch_edge_ports(sdnr_ctx *ctx, const uint64_t *d_ends, int32_t nends,
+                           const uint64_t *d_ports, int32_t nports, uint8_t *d_is_edge)
+{
+    if (nports == 0) return SDNR_OK;
+    int g = (nports + 255) / 256;
+    if (g > ctx->num_cus * 8) g = ctx->num_cus * 8;
+    ctx->last_kernel = "edge_port_kernel";
+    if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
+    hipLaunchKernelGGL(edge_port_kernel, dim3(g), dim3(256), 0, ctx->stream, d_ends, nends, d_ports,
+                       nports, d_is_edge);
     SDNR_HIP(hipGetLastError());
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
     return SDNR_OK;

@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = (
     "sdnr_graph_info", "sdnr_dfs_tables", "sdnr_dfs_tables_packed", "sdnr_shortest_tables",
     "sdnr_apsp", "sdnr_route_offsets", "sdnr_route_expand", "sdnr_ecmp_counts",
     "sdnr_ecmp_routes",
-    "sdnr_last_kernel_ms", "sdnr_last_kernel", "sdnr_last_launches",
+    "sdnr_last_kernel_ms", "sdnr_last_kernel", "sdnr_last_launches", "sdnr_edge_ports",
 )
 
 
@@ -84,6 +84,7 @@ def _bind(L):
         "sdnr_last_kernel_ms": ([vp, ctypes.POINTER(ctypes.c_float)], c_int),
         "sdnr_last_kernel": ([vp], ctypes.c_char_p),
         "sdnr_last_launches": ([vp, ctypes.POINTER(i32)], c_int),
+        "sdnr_edge_ports": ([vp, vp, i32, vp, i32, vp, u32], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -315,6 +316,16 @@ class Context(object):
                                            ctypes.c_void_p(dsts_ptr), ctypes.c_void_p(last_ptr),
                                            int(npairs), ctypes.c_void_p(off_ptr),
                                            ctypes.c_void_p(sw_ptr), ctypes.c_void_p(hp_ptr), flags))
+
+    def edge_ports(self, ends, ports):
+        """bool [n_ports]: ports (uint64 keys) that are no link end (``ends``:
+        sorted uint64 keys), see sdnr_edge_ports."""
+        ends = np.ascontiguousarray(ends, np.uint64)
+        ports = np.ascontiguousarray(ports, np.uint64)
+        out = np.empty(ports.shape[0], np.uint8)
+        _check(self._lib.sdnr_edge_ports(self._h, _ptr(ends), int(ends.shape[0]), _ptr(ports),
+                                         int(ports.shape[0]), _ptr(out), 0))
+        return out.astype(bool)
 
     def apsp(self):
         dist = np.empty((self.V, self.V), np.uint16)

@@ -218,6 +218,11 @@ class RouteEngine(object):
         self.ctx.synchronize()
         return off, sw[:total].cpu().numpy(), hp[:total].cpu().numpy()
 
+    def edge_ports(self, ends, ports):
+        """Flood-port mask (sdnr_edge_ports, reference topology.py:150-155):
+        bool [n] -- ``ports`` keys that are no link end (``ends`` sorted)."""
+        return self.ctx.edge_ports(ends, ports)
+
     def close(self):
         self.ctx.close()
 

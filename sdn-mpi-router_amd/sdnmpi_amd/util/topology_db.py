@@ -67,7 +67,7 @@ class TopologyDB(object):
         self._export = None
         self._cache = None
         self._hv = (None, None)          # (version key, host vertices)
-        self._lp = (None, None)          # (links version, link endpoint ports)
+        self._em = (None, None)          # (links/switches version, edge-port state)
         # Switch DPID -> Switch; src DPID -> dst DPID -> Link; MAC -> Host
         self.switches = {}
         self.links = {}
@@ -235,31 +235,65 @@ class TopologyDB(object):
         return out
 
     # -- flood helper --------------------------------
-    def _link_ports(self):
-        """{(dpid, port_no)} of every link endpoint, rebuilt when ``links``
-        changes (one pass over the links instead of one per query)."""
-        key = self._versions.links
-        if self._lp[0] != key:
+    def _edge_state(self):
+        """(sorted link-end keys, {(dpid, port_no): is_edge} of every switch
+        port) for the current links/switches, from one device pass
+        (sdnr_edge_ports) per version instead of the reference's scan over
+        every link per port.  Keys: dense switch id << 32 | port_no."""
+        key = (self._versions.links, self._versions.switches)
+        if self._em[0] != key:
+            idx = self.graph().index
             ends = set()
             for nb in self.links.values():
                 for lk in nb.values():
-                    ends.add((lk.src.dpid, lk.src.port_no))
-                    ends.add((lk.dst.dpid, lk.dst.port_no))
-            self._lp = (key, ends)
-        return self._lp[1]
+                    for p in (lk.src, lk.dst):
+                        d = idx.get(p.dpid)
+                        if d is not None:
+                            ends.add((d << 32) | (int(p.port_no) & 0xFFFFFFFF))
+            ends = np.asarray(sorted(ends), np.uint64)
+            ports, keys = [], []
+            for sw in self.switches.values():
+                for p in getattr(sw, "ports", ()):
+                    d = idx.get(p.dpid)
+                    if d is not None:
+                        ports.append((p.dpid, p.port_no))
+                        keys.append((d << 32) | (int(p.port_no) & 0xFFFFFFFF))
+            mask = self.engine.edge_ports(ends, np.asarray(keys, np.uint64)) if keys else []
+            self._em = (key, (ends, dict(zip(ports, (bool(m) for m in mask)))))
+        return self._em[1]
 
     def is_edge_port(self, port):
         """``TopologyManager._is_edge_port`` (reference sdnmpi/topology.py:
-        150-155): the port is neither end of any link.  O(1) per query."""
-        return (port.dpid, port.port_no) not in self._link_ports()
+        150-155): the port is neither end of any link."""
+        ends, known = self._edge_state()
+        hit = known.get((port.dpid, port.port_no))
+        if hit is not None:
+            return hit
+        d = self.graph().index.get(port.dpid)
+        if d is None:                     # not a switch of the graph: no link end
+            return True
+        k = np.asarray([(d << 32) | (int(port.port_no) & 0xFFFFFFFF)], np.uint64)
+        return bool(self.engine.edge_ports(ends, k)[0])
 
     def edge_ports(self, switch, in_port=None):
         """The ports ``_do_broadcast`` floods on ``switch`` (topology.py:
         157-168): edge ports that are not reserved, minus ``in_port``."""
-        ends = self._link_ports()
         return [p for p in switch.ports
-                if (p.dpid, p.port_no) not in ends and not p.is_reserved()
+                if self.is_edge_port(p) and not p.is_reserved()
                 and (in_port is None or p.port_no != in_port)]
+
+    def broadcast_ports(self, dpid, in_port):
+        """{switch dpid: [port_no, ...]} -- every OFPActionOutput
+        ``_do_broadcast(data, dpid, in_port)`` emits (topology.py:157-177):
+        each switch's non-reserved edge ports, the ingress port excluded on
+        the switch the packet came from."""
+        _, known = self._edge_state()
+        out = {}
+        for sw in self.switches.values():
+            out[sw.dp.id] = [p.port_no for p in sw.ports
+                             if known.get((p.dpid, p.port_no), True) and not p.is_reserved()
+                             and not (sw.dp.id == dpid and p.port_no == in_port)]
+        return out
 
     # -- batched (all-pairs) interface ---------------------------------
     def route_tables(self, mode="dfs", vertices=None):

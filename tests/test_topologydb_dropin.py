@@ -167,6 +167,10 @@ class _FakeEngine(object):
             out.append(np.asarray(q, np.int32).reshape(len(q), -1))
         return out
 
+    def edge_ports(self, ends, ports):
+        # membership test of routes.hip's edge_port_kernel (test double only)
+        return ~np.isin(np.asarray(ports, np.uint64), np.asarray(ends, np.uint64))
+
     def expand(self, export, tables, rows, dsts, last_port):
         # numpy restatement of routes.hip (test double only)
         from sdnmpi_amd.engine import expand_tree_paths
@@ -368,8 +372,20 @@ def test_ecmp_sets_k48_sampled():
 
 
 def test_edge_port_helpers_match_reference_loop():
-    """is_edge_port / edge_ports vs the reference's O(links) loop
-    (sdnmpi/topology.py:150-168), before and after link changes."""
+    _edge_port_replay(_FakeEngine())
+
+
+@pytest.mark.gpu
+def test_edge_port_helpers_gpu():
+    """The device flood-port mask (sdnr_edge_ports) against the reference's
+    loop through link deletions and whole-entry removal."""
+    _edge_port_replay(None)
+
+
+def _edge_port_replay(engine):
+    """is_edge_port / edge_ports / broadcast_ports vs the reference's
+    O(links) loop (sdnmpi/topology.py:150-177), before and after link
+    changes."""
     from sdnmpi_amd import topologies as T
     from sdnmpi_amd.objects import Switch
 
@@ -382,6 +398,8 @@ def test_edge_port_helpers_match_reference_loop():
 
     fabric = T.fat_tree(4)
     db = fabric.populate(TopologyDB())
+    if engine is not None:
+        db._engine = engine
     ports = {}
     for nb in db.links.values():
         for lk in nb.values():
@@ -401,7 +419,18 @@ def test_edge_port_helpers_match_reference_loop():
             want = [p for p in sw.ports if ref_is_edge(db, p) and not p.is_reserved()
                     and p.port_no != 3]
             assert db.edge_ports(sw, in_port=3) == want
+        # _do_broadcast(data, dpid, in_port) over every switch
+        src = sws[1].dp.id
+        bc = db.broadcast_ports(src, 1)
+        for sw in sws:
+            want = [p.port_no for p in sw.ports if ref_is_edge(db, p) and not p.is_reserved()
+                    and not (sw.dp.id == src and p.port_no == 1)]
+            assert bc[sw.dp.id] == want
+        # a port of no switch object (reference: any Port works)
+        assert db.is_edge_port(Port(sws[0].dp.id, 999)) is True
 
+    for sw in sws:
+        db.add_switch(sw)
     check()
     lk = next(iter(db.links[sws[-1].dp.id].values()))
     db.delete_link(lk)
