@@ -19,5 +19,6 @@ run dragonfly:16,8,8 dfs 10 2
 run dragonfly:16,8,8 shortest 5 1 --no-cpu-baseline
 TMO=600 run torus:32,32,32 dfs 2 1 --cpu-budget-s 8
 TMO=600 run torus:32,32,32 shortest 2 1 --no-cpu-baseline
-TMO=900 run jellyfish:100000,16,1 dfs 1 1 --cpu-budget-s 8
+TMO=900 run jellyfish:100000,16,1 dfs 2 1 --cpu-budget-s 8
+TMO=900 run jellyfish:100000,16,1 shortest 3 1 --no-cpu-baseline
 exit 0
