@@ -744,15 +744,31 @@ __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
     }
 }
 
-// decode the planes of one batch into 64 table rows, coalesced along x
+// decode the planes of one batch into 64 table rows, coalesced along x; the
+// block's ELL rows (neighbour ids and ports, 256 vertices) are staged in LDS
+// once, transposed to [slot][vertex] so the per-destination lookups of a
+// wave hit 32 different banks, instead of two scattered global loads per
+// (destination, vertex)
 template <int SB>
 __global__ __launch_bounds__(256) void msbfs_plane_tables_kernel(
     int V, int W, const int32_t *__restrict__ ell_col, const int32_t *__restrict__ ell_port,
     int ndst, const uint64_t *__restrict__ pl, uint16_t *__restrict__ dist,
     int32_t *__restrict__ nh, int32_t *__restrict__ nh_port)
 {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    extern __shared__ int32_t lrow[];          // [2][W][256]: ids, ports
+    const int x0 = blockIdx.x * blockDim.x;
+    const int t = threadIdx.x;
+    const int x = x0 + t;
     const int batch = blockIdx.y;
+    const int nx = min(256, V - x0);
+    if (nh) {
+        for (int e = t; e < nx * W; e += 256) {   // coalesced reads of the block's rows
+            const int xl = e / W, j = e - xl * W;
+            lrow[j * 256 + xl] = ell_col[(size_t)x0 * W + e];
+            lrow[(W + j) * 256 + xl] = ell_port[(size_t)x0 * W + e];
+        }
+        __syncthreads();
+    }
     if (x >= V) return;
     const uint64_t *b = pl + (size_t)batch * kPlanes * V;
     const uint64_t vx = b[(size_t)kPlVis * V + x];
@@ -770,12 +786,12 @@ __global__ __launch_bounds__(256) void msbfs_plane_tables_kernel(
             L = 0;
 #pragma unroll
             for (int k = 0; k < 8; ++k) L |= (uint32_t)((d[k] >> i) & 1ull) << k;
-            if (L) {
+            if (L && nh) {
                 int sl = 0;
 #pragma unroll
                 for (int k = 0; k < SB; ++k) sl |= (int)((s[k] >> i) & 1ull) << k;
-                best = ell_col[(size_t)x * W + sl];
-                if (nh_port) bport = ell_port[(size_t)x * W + sl];
+                best = lrow[sl * 256 + t];
+                bport = lrow[(W + sl) * 256 + t];
             }
         }
         dist[row] = (uint16_t)L;
@@ -861,16 +877,17 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
         uint16_t *dist = d_dist + (size_t)c0 * 64 * V;
         int32_t *nh = d_nh ? d_nh + (size_t)c0 * 64 * V : nullptr;
         int32_t *nhp = d_nh_port ? d_nh_port + (size_t)c0 * 64 * V : nullptr;
+        const size_t tl = d_nh ? (size_t)2 * W * 256 * sizeof(int32_t) : 0;
         if (sb == 3)
-            hipLaunchKernelGGL(msbfs_plane_tables_kernel<3>, dim3(gx, nbc), dim3(256), 0,
+            hipLaunchKernelGGL(msbfs_plane_tables_kernel<3>, dim3(gx, nbc), dim3(256), tl,
                                ctx->stream, V, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
                                nhp);
         else if (sb == 4)
-            hipLaunchKernelGGL(msbfs_plane_tables_kernel<4>, dim3(gx, nbc), dim3(256), 0,
+            hipLaunchKernelGGL(msbfs_plane_tables_kernel<4>, dim3(gx, nbc), dim3(256), tl,
                                ctx->stream, V, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
                                nhp);
         else
-            hipLaunchKernelGGL(msbfs_plane_tables_kernel<5>, dim3(gx, nbc), dim3(256), 0,
+            hipLaunchKernelGGL(msbfs_plane_tables_kernel<5>, dim3(gx, nbc), dim3(256), tl,
                                ctx->stream, V, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
                                nhp);
         SDNR_HIP(hipGetLastError());
