@@ -1053,6 +1053,11 @@ __global__ __launch_bounds__(64) void dfs_global_packed_kernel(
 // ---------------------------------------------------------------------------
 constexpr int kRow32 = 0, kRow16 = 1, kRow17 = 2;
 constexpr int kSplitQ = 64;                    // queued records per search wave
+// SDNROUTE_DFS_FLAGS (tuning): search waves at raised issue priority,
+// non-temporal table stores, or (diagnostic) no table stores at all / port
+// slot instead of the port
+// (diagnostic) no port lookups in the writer
+constexpr int kFlagPrio = 1, kFlagNT = 2, kFlagNoStore = 4, kFlagNoPort = 8;
 
 template <int FMT>
 __device__ __forceinline__ int split_row(const void *__restrict__ rows,
@@ -1074,10 +1079,28 @@ __device__ __forceinline__ int split_row(const void *__restrict__ rows,
 // apart -- a 32^3 torus's z neighbours) fall in different LDS banks
 __device__ __forceinline__ int vsw(int w) { return w ^ ((w >> 5) & 31); }
 
-__host__ __device__ inline size_t split_lds_words(int V, int ring, int ns, bool hops)
+// stack ring entries: (vertex, depth), or the vertex alone (half the LDS:
+// more sources per CU on the 100k Jellyfish, 10 instead of 9; measured 13 %
+// slower on the torus, which keeps the pair)
+template <bool HOPS> struct SplitRing;
+template <> struct SplitRing<true> {
+    using T = uint2;
+    static __device__ __forceinline__ uint2 get(T e) { return e; }
+    static __device__ __forceinline__ T put(uint32_t v, uint32_t d) { return make_uint2(v, d); }
+};
+template <> struct SplitRing<false> {
+    using T = uint32_t;
+    static __device__ __forceinline__ uint2 get(T e) { return make_uint2(e, 0u); }
+    static __device__ __forceinline__ T put(uint32_t v, uint32_t) { return v; }
+};
+
+__host__ __device__ constexpr bool split_wide_ring(int lpr, bool hops) { return hops || lpr == 8; }
+
+__host__ __device__ inline size_t split_lds_words(int V, int ring, int ns, bool hops, int lpr)
 {
     const size_t VWp = (size_t)((((V + 31) >> 5) + 31) & ~31);
-    return (size_t)ns * (VWp + 2 * (size_t)ring) + (size_t)ns * kSplitQ * (hops ? 3 : 2) +
+    return (size_t)ns * (VWp + (split_wide_ring(lpr, hops) ? 2 : 1) * (size_t)ring) +
+           (size_t)ns * kSplitQ * (hops ? 3 : 2) +
            ((3 * (size_t)ns + 3) & ~(size_t)3);
 }
 
@@ -1086,7 +1109,8 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
     int V, int W, const void *__restrict__ rows, const uint32_t *__restrict__ rhi,
     const int32_t *__restrict__ ell_port, const int32_t *__restrict__ src, int nsrc,
     int32_t *__restrict__ out_parent, int32_t *__restrict__ out_port,
-    int32_t *__restrict__ out_hops, uint2 *__restrict__ spill_all, int *__restrict__ err)
+    int32_t *__restrict__ out_hops, uint2 *__restrict__ spill_all, int *__restrict__ err,
+    int flags)
 {
     constexpr int R = 64 / LPR;
     constexpr int K = R * J;
@@ -1096,7 +1120,10 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int VW = (V + 31) >> 5;
     const int VWp = (VW + 31) & ~31;          // whole 32-word blocks (swizzled)
-    const int per = VWp + 2 * RING;           // words per search wave: vis | stack ring
+    constexpr bool WR = split_wide_ring(LPR, HOPS);
+    using RE = SplitRing<WR>;
+    using RT = typename RE::T;
+    const int per = VWp + (WR ? 2 : 1) * RING;   // words per search wave: vis | stack ring
     uint2 *qrec = reinterpret_cast<uint2 *>(lds + NS * per);
     uint32_t *qdep = reinterpret_cast<uint32_t *>(qrec + NS * kSplitQ);
     // ctl[k] records published by search wave k, ctl[NS + k] records the
@@ -1110,16 +1137,22 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
 
     if (w < NS) {
         // ------------------------------------------------------ a search wave
+        if (flags & kFlagPrio) __builtin_amdgcn_s_setprio(3);
         const int pos = lane % LPR;
         const int sub = lane / LPR;
         const uint64_t lowmask = (LPR == 64) ? ~0ull : ((1ull << LPR) - 1ull);
         uint32_t *vis = lds + w * per;
-        uint2 *ring = reinterpret_cast<uint2 *>(vis + VWp);   // (v, depth)
+        RT *ring = reinterpret_cast<RT *>(vis + VWp);   // (v[, depth])
         uint2 *q = qrec + w * kSplitQ;
         uint32_t *qd = qdep + w * kSplitQ;
         const int slot_id = blockIdx.x * NS + w;
-        uint2 *spill = spill_all + (size_t)slot_id * (size_t)V;
+        RT *spill = reinterpret_cast<RT *>(spill_all) + (size_t)slot_id * (size_t)V;
         int pub = 0, cons = 0;
+#ifdef SDNR_STAMPS
+        unsigned long long z_t0, z_t1, z_a, z_b, z_c, z_rd = 0, z_qw = 0, z_push = 0, z_it = 0,
+                                                   z_nl = 0, z_sp = 0, z_rf = 0, z_rfc = 0;
+        SDNR_STAMP(z_t0);
+#endif
         for (int si = slot_id; si < nsrc; si += gridDim.x * NS) {
             const int s = uniform(src[si]);
             int32_t *prow = out_parent + (size_t)si * V;
@@ -1139,7 +1172,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                 prow[s] = PACKED ? (int32_t)((uint32_t)s | 0xFFFF0000u) : s;
                 if (!PACKED) trow[s] = -1;
                 if (HOPS) hrow[s] = 0;
-                ring[0] = make_uint2((uint32_t)s, 0u);
+                ring[0] = RE::put((uint32_t)s, 0u);
                 __hip_atomic_store(&ctl[2 * NS + w], si, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
             }
@@ -1151,11 +1184,23 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                     const int n = gsp < RING / 2 ? gsp : RING / 2;
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // own spill stores
                     bot = (bot - n) & (RING - 1);
+#ifdef SDNR_STAMPS
+                    SDNR_STAMP(z_a);
+#endif
                     for (int i = lane; i < n; i += SDNR_WAVE)
                         ring[(bot + i) & (RING - 1)] = spill[gsp - n + i];
                     gsp -= n;
                     lsp = n;
+#ifdef SDNR_STAMPS
+                    SDNR_STAMP(z_b);
+                    z_rf++;
+                    z_rfc += z_b - z_a;
+#endif
                 }
+#ifdef SDNR_STAMPS
+                SDNR_STAMP(z_a);
+                z_it++;
+#endif
                 const int kk = lsp < K ? lsp : K;
                 // every lane reads its slot's stack entry itself (no
                 // cross-lane shuffle on the chain); slots past the stack
@@ -1165,15 +1210,15 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                 uint2 ue[J];
                 int x[J];
                 if (J == 1) {
-                    ue[0] = ring[(bot + lsp - 1 - sub) & (RING - 1)];
+                    ue[0] = RE::get(ring[(bot + lsp - 1 - sub) & (RING - 1)]);
                     ue[0].x = sub < kk ? ue[0].x : 0u;
                 } else {
-                    uint2 me = ring[(bot + lsp - 1 - lane) & (RING - 1)];
+                    uint2 me = RE::get(ring[(bot + lsp - 1 - lane) & (RING - 1)]);
                     me.x = lane < kk ? me.x : 0u;
 #pragma unroll
                     for (int j = 0; j < J; ++j) {
                         ue[j].x = (uint32_t)__shfl((int)me.x, j * R + sub);
-                        ue[j].y = (uint32_t)__shfl((int)me.y, j * R + sub);
+                        ue[j].y = WR ? (uint32_t)__shfl((int)me.y, j * R + sub) : 0u;
                     }
                 }
 #pragma unroll
@@ -1203,6 +1248,10 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
 #pragma unroll
                 for (int j = J - 1; j >= 0; --j)
                     if (m[j] != 0) jstar = j;
+#ifdef SDNR_STAMPS
+                SDNR_STAMP(z_b);
+                z_rd += z_b - z_a;
+#endif
                 if (jstar == J) {
                     lsp -= kk;
                     continue;
@@ -1221,7 +1270,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                 const int istar = jstar * R + sstar;
                 const uint64_t mm = mj & (lowmask << (sstar * LPR));
                 const int eu = read_lane((int)uj.x, sstar * LPR);
-                const uint32_t ed = (uint32_t)read_lane((int)uj.y, sstar * LPR);
+                const uint32_t ed = WR ? (uint32_t)read_lane((int)uj.y, sstar * LPR) : 0u;
                 lsp -= istar + 1;
                 const int cnt = __popcll(mm);
                 // room in the record queue (the writer publishes its progress)
@@ -1243,6 +1292,12 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                         __builtin_amdgcn_s_sleep(1);
                     }
                 }
+#ifdef SDNR_STAMPS
+                SDNR_STAMP(z_c);
+                z_qw += z_c - z_b;
+                z_nl++;
+                if (lsp + cnt > RING) z_sp++;
+#endif
                 if (lsp + cnt > RING) {            // spill the oldest half
                     for (int i = lane; i < RING / 2; i += SDNR_WAVE)
                         spill[gsp + i] = ring[(bot + i) & (RING - 1)];
@@ -1256,10 +1311,14 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                     q[(pub + rank) & (kSplitQ - 1)] =
                         make_uint2((uint32_t)vv | ((uint32_t)pos << 26), (uint32_t)eu);
                     if (HOPS) qd[(pub + rank) & (kSplitQ - 1)] = ed + 1u;
-                    ring[(bot + lsp + rank) & (RING - 1)] = make_uint2((uint32_t)vv, ed + 1u);
+                    ring[(bot + lsp + rank) & (RING - 1)] = RE::put((uint32_t)vv, ed + 1u);
                 }
                 lsp += cnt;
                 pub += cnt;
+#ifdef SDNR_STAMPS
+                SDNR_STAMP(z_a);
+                z_push += z_a - z_c;
+#endif
             }
             if (pub != pubd) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -1289,6 +1348,20 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         if (lane == 0) __hip_atomic_store(&ctl[2 * NS + w], -1, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef SDNR_STAMPS
+        SDNR_STAMP(z_t1);
+        if (lane == 0) {
+            atomicAdd(&g_stamp[0], z_t1 - z_t0);   // search wave lifetime
+            atomicAdd(&g_stamp[1], z_rd);          // stack + row + visited per iteration
+            atomicAdd(&g_stamp[2], z_it);          // iterations
+            atomicAdd(&g_stamp[3], z_nl);          // non-leaf pops
+            atomicAdd(&g_stamp[4], z_qw);          // queue-room waits
+            atomicAdd(&g_stamp[5], z_push);        // push (+ spill)
+            atomicAdd(&g_stamp[6], z_sp);          // spills
+            atomicAdd(&g_stamp[7], z_rf);          // refills
+            atomicAdd(&g_stamp[8], z_rfc);         // refill cycles
+        }
+#endif
     } else {
         // ------------------------------------------------------ the writer
         int consd[NS];
@@ -1316,16 +1389,30 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                         const uint2 r = qrec[at];
                         const int v = (int)(r.x & 0x3FFFFFFu), slot = (int)(r.x >> 26);
                         const int par = (int)r.y;
-                        const int pt = ell_port[(size_t)par * W + slot];
+                        const int pt = (flags & kFlagNoPort) ? slot : ell_port[(size_t)par * W + slot];
                         const size_t e = (size_t)row * V + v;
-                        if (PACKED) {
-                            out_parent[e] = (int32_t)(((uint32_t)par & 0xFFFFu) |
-                                                      ((uint32_t)pt << 16));
+                        if (flags & kFlagNoStore) {
+                            // diagnostic: records consumed, no table stores
+                        } else if (flags & kFlagNT) {
+                            if (PACKED) {
+                                __builtin_nontemporal_store(
+                                    (int32_t)(((uint32_t)par & 0xFFFFu) | ((uint32_t)pt << 16)),
+                                    &out_parent[e]);
+                            } else {
+                                __builtin_nontemporal_store(par, &out_parent[e]);
+                                __builtin_nontemporal_store(pt, &out_port[e]);
+                            }
+                            if (HOPS) __builtin_nontemporal_store((int)qdep[at], &out_hops[e]);
                         } else {
-                            out_parent[e] = par;
-                            out_port[e] = pt;
+                            if (PACKED) {
+                                out_parent[e] = (int32_t)(((uint32_t)par & 0xFFFFu) |
+                                                          ((uint32_t)pt << 16));
+                            } else {
+                                out_parent[e] = par;
+                                out_port[e] = pt;
+                            }
+                            if (HOPS) out_hops[e] = (int)qdep[at];
                         }
-                        if (HOPS) out_hops[e] = (int)qdep[at];
                     }
                     consd[k] = C + n;
                     // the record reads above are done (LDS ops in order)
@@ -1378,7 +1465,8 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
     const uint32_t *__restrict__ deg, const int32_t *__restrict__ row_ptr,
     const int32_t *__restrict__ port, int W, const int32_t *__restrict__ ell_port,
     const int32_t *__restrict__ src, int nsrc, int32_t *__restrict__ out_parent,
-    int32_t *__restrict__ out_port, int32_t *__restrict__ out_hops, int *__restrict__ err)
+    int32_t *__restrict__ out_port, int32_t *__restrict__ out_hops, int *__restrict__ err,
+    int flags)
 {
     static_assert(NW >= 2, "wave 0 searches, the others decrement");
     constexpr int U = 4;                         // init / flush vertices per thread per step
@@ -1447,6 +1535,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
 
         if (w == 0) {
             // ------------------------------------------------ the search
+            if (flags & kFlagPrio) __builtin_amdgcn_s_setprio(3);
             if (lane == 0) {
                 vis[s >> 5] |= 1u << (s & 31);
                 vis[V >> 5] |= 1u << (V & 31);
@@ -1560,6 +1649,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (flags & kFlagPrio) __builtin_amdgcn_s_setprio(0);
 #ifdef SDNR_STAMPS
             SDNR_STAMP(st_t1);
             if (lane == 0) {
@@ -1884,6 +1974,12 @@ static int dfs_batch_depth(const sdnr_ctx *ctx)
     return ctx->max_deg >= 12 ? 16 : 8;
 }
 
+static int dfs_flags()
+{
+    const char *f = getenv("SDNROUTE_DFS_FLAGS");
+    return f ? atoi(f) : 0;
+}
+
 // SDNROUTE_DFS_SPLIT=0 keeps the single-wave lane-packed kernel (A/B, tests)
 static bool split_ok()
 {
@@ -1904,12 +2000,30 @@ static int launch_split(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, int32
                         int32_t *d_port, int32_t *d_hops, uint32_t *d_tree)
 {
     int ns = ctx->W <= 8 && packed_j8(ctx->V) == 1 ? 7 : 3;
+    if (ctx->W > 8 && ctx->W <= 16) {
+        // rows of 9-16 slots (Jellyfish): 3 or 5 sources per workgroup,
+        // whichever keeps more sources resident per CU (100k Jellyfish
+        // without hop counts: 2 x 5 = 10 vs 3 x 3 = 9, measured 5 % faster)
+        const bool hops = d_hops != nullptr;
+        auto per_cu = [&](int k) {
+            const size_t l = split_lds_words(ctx->V, 512, k, hops, 16) * 4;
+            size_t b = SDNR_LDS_PER_CU / l;
+            if (b > (size_t)(32 / (k + 1))) b = 32 / (k + 1);
+            return (size_t)k * b;
+        };
+        if (per_cu(5) > per_cu(3)) ns = 5;
+    }
     if (const char *f = getenv("SDNROUTE_DFS_SPLIT_NS")) {
         const int k = atoi(f);
         if (k == 3 || k == 7) ns = k;
+        if ((k == 5 || k == 11) && ctx->W > 8 && ctx->W <= 16) ns = k;   // rows of 9-16 slots
     }
-    return ns == 7 ? launch_split_ns<7>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree)
-                   : launch_split_ns<3>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree);
+    switch (ns) {
+    case 7: return launch_split_ns<7>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree);
+    case 5: return launch_split_ns<5>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree);
+    case 11: return launch_split_ns<11>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree);
+    default: return launch_split_ns<3>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree);
+    }
 }
 
 template <int NS>
@@ -1922,11 +2036,15 @@ static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, in
     const int j8 = packed_j8(V);
     // stack ring: 128 entries on sparse tori (more sources per CU), 512 for
     // rows of 9-32 slots (Jellyfish: 3 workgroups of 3 sources per CU)
-    const int ring = lpr == 8 ? (j8 == 1 ? 128 : 1024) : 512;
+    int ring = lpr == 8 ? (j8 == 1 ? 128 : 1024) : 512;
+    if (const char *f = getenv("SDNROUTE_DFS_SPLIT_RING"))   // rows of 9-16 slots
+        if (lpr == 16 && !strcmp(f, "256")) ring = 256;
+    constexpr bool kWide = NS == 5 || NS == 11;   // only for rows of 9-16 slots
+    if (kWide && lpr != 16) return sdnr_fail(SDNR_ERR_INVAL, "dfs split: NS=%d needs rows of 9-16 slots", NS);
     const int fmt = ctx->ell16 && V <= 65535 ? kRow16 : (ctx->ell16 && ctx->ell_hi ? kRow17 : kRow32);
     if (packed && fmt != kRow16)
         return sdnr_fail(SDNR_ERR_INVAL, "dfs split: packed tables need V <= 65535");
-    const size_t lds = split_lds_words(V, ring, NS, hops) * 4;
+    const size_t lds = split_lds_words(V, ring, NS, hops, lpr) * 4;
     if (lds > SDNR_MAX_LDS_PER_BLOCK)
         return sdnr_fail(SDNR_ERR_INVAL, "graph too large for the LDS visited sets (V=%d)", V);
     size_t bpc = SDNR_LDS_PER_CU / lds;
@@ -1952,7 +2070,7 @@ static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, in
         sdnr_allow_lds(reinterpret_cast<const void *>(k), lds);                              \
         hipLaunchKernelGGL(k, dim3(grid), dim3((NS + 1) * 64), lds, ctx->stream, V, W, rows, \
                            ctx->ell_hi, ctx->ell_port, d_src, nsrc, par, d_port, d_hops,     \
-                           spill, ctx->d_err);                                               \
+                           spill, ctx->d_err, dfs_flags());                                  \
     } while (0)
 #define SDNR_SPLIT_F(L_, J_, R_, H_)                                                          \
     do {                                                                                     \
@@ -1965,10 +2083,16 @@ static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, in
     do {                                                                                     \
         if (hops) SDNR_SPLIT_F(L_, J_, R_, true); else SDNR_SPLIT_F(L_, J_, R_, false);      \
     } while (0)
-    if (lpr == 8 && ring == 128) SDNR_SPLIT_H(8, 1, 128);
-    else if (lpr == 8) SDNR_SPLIT_H(8, 2, 1024);
-    else if (lpr == 16) SDNR_SPLIT_H(16, 4, 512);
-    else SDNR_SPLIT_H(32, 8, 512);
+    if constexpr (kWide) {
+        if (ring == 256) SDNR_SPLIT_H(16, 4, 256);
+        else SDNR_SPLIT_H(16, 4, 512);
+    } else {
+        if (lpr == 8 && ring == 128) SDNR_SPLIT_H(8, 1, 128);
+        else if (lpr == 8) SDNR_SPLIT_H(8, 2, 1024);
+        else if (lpr == 16 && ring == 256) SDNR_SPLIT_H(16, 4, 256);
+        else if (lpr == 16) SDNR_SPLIT_H(16, 4, 512);
+        else SDNR_SPLIT_H(32, 8, 512);
+    }
 #undef SDNR_SPLIT_H
 #undef SDNR_SPLIT_F
 #undef SDNR_SPLIT
@@ -2064,7 +2188,7 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
                            ctx->radj16, ctx->deg32, ctx->row_ptr, ctx->port, ctx->W,         \
                            ctx->ell_port, d_src, nsrc,                                       \
                            P_ ? reinterpret_cast<int32_t *>(d_tree) : d_parent, d_port,      \
-                           d_hops, err);                                                     \
+                           d_hops, err, dfs_flags());                                        \
     } while (0)
 #define SDNR_ASYNC(N_, H_) SDNR_ASYNC_P(N_, H_, false)
         if (packed) {

@@ -152,12 +152,15 @@ def test_dfs_fullsize_all_host_sources(ctx, name):
     _check_pairs(g, fabric, p, t, srcs)
 
 
-@pytest.mark.parametrize("split", ["1", "0", "ns3", "ns7"])
+@pytest.mark.parametrize("split", ["1", "0", "ns3", "ns7", "ns5", "ns5-ring256", "ns11-ring256"])
 @pytest.mark.parametrize("name,nsample", [("torus_32x32x32_sample", 384),
                                           ("jellyfish_n100000_r16_sample", 48)])
 def test_dfs_fullsize_sampled_sources(ctx, monkeypatch, name, nsample, split):
     if split.startswith("ns"):                   # search waves per workgroup
-        monkeypatch.setenv("SDNROUTE_DFS_SPLIT_NS", split[2:])
+        ns, _, ring = split[2:].partition("-ring")
+        monkeypatch.setenv("SDNROUTE_DFS_SPLIT_NS", ns)
+        if ring:
+            monkeypatch.setenv("SDNROUTE_DFS_SPLIT_RING", ring)
     else:
         monkeypatch.setenv("SDNROUTE_DFS_SPLIT", split)
     g = G.Golden(name)
