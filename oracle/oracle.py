@@ -229,6 +229,30 @@ def _shortest_paths_lex(links, s, d):
     return out
 
 
+def ecmp_counts(csr, dist_row):
+    """Number of routes find_route(src, dst, multiple=True) returns from every
+    vertex toward one destination (topology_db.py:86-122 enumerates every
+    shortest simple path; their number is the count of shortest-path DAG
+    walks): a level DP over dist_row (hops x -> dst, 0xFFFF unreachable, from
+    dest_tables), in Python integers, saturated at 2**64-1 as the device's
+    u64 counts are.  Pinned by tests/test_oracle_golden.py against the sizes
+    of the reference's own multiple=True outputs."""
+    V = csr.V
+    order = sorted((int(dist_row[x]), x) for x in range(V) if dist_row[x] != 0xFFFF)
+    cnt = [0] * V
+    for dx, x in order:
+        if dx == 0:
+            cnt[x] = 1
+            continue
+        c = 0
+        for e in range(int(csr.row_ptr[x]), int(csr.row_ptr[x + 1])):
+            n = int(csr.col[e])
+            if dist_row[n] != 0xFFFF and int(dist_row[n]) + 1 == dx:
+                c += cnt[n]
+        cnt[x] = c
+    return np.array([min(c, 2**64 - 1) for c in cnt], dtype=np.uint64)
+
+
 def find_routes_all_shortest(db, src_mac, dst_mac):
     """find_route(src_mac, dst_mac, multiple=True), reference semantics."""
     ep = _endpoints(db, src_mac, dst_mac)

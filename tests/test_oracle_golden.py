@@ -103,6 +103,26 @@ def test_multiple_routes_match_reference(name):
 
 
 @pytest.mark.parametrize("name", G.MULTI)
+def test_ecmp_counts_match_reference(name):
+    """oracle.ecmp_counts == the number of routes the reference returned for
+    every multiple=True fixture pair."""
+    g = G.Golden(name)
+    fabric = g.fabric()
+    csr = fabric.csr()
+    hv, _ = fabric.host_table()
+    dsts = np.unique(hv)
+    dist, _, _ = O.dest_tables(csr, dsts)
+    drow = {int(d): i for i, d in enumerate(dsts)}
+    counts = {}
+    for i in range(len(g)):
+        a, b = int(g.pair_src[i]), int(g.pair_dst[i])
+        d = int(hv[b])
+        if d not in counts:
+            counts[d] = O.ecmp_counts(csr, dist[drow[d]])
+        assert int(counts[d][int(hv[a])]) == len(g.multi(i)), (name, i)
+
+
+@pytest.mark.parametrize("name", G.MULTI)
 def test_bfs_tree_is_lexmin_shortest(name):
     """Per-source FIFO-BFS tree path == routes[0] of multiple=True."""
     g = G.Golden(name)
