@@ -57,12 +57,17 @@ def parse():
     ap.add_argument("--ranks", type=int, default=1024,
                     help="flows mode: MPI ranks placed on random hosts; every ordered "
                          "rank pair's flow entries are emitted per step")
-    ap.add_argument("--layout", choices=["auto", "packed", "int32"], default="auto",
+    ap.add_argument("--layout", choices=["auto", "packed", "slots", "int32"], default="auto",
                     help="dfs tables: packed u32 (parent | port << 16) when the fabric "
-                         "allows it (V <= 65535, 16-bit ports), else int32 parent + port")
+                         "allows it (V <= 65535, 16-bit ports), else slot trees (parent | "
+                         "slot << 26, sdnr_dfs_tables_slots) when rows have <= 63 links, "
+                         "else int32 parent + port")
     ap.add_argument("--max-sources", type=int, default=0,
                     help="dfs/shortest: only the first N sources/destinations (probes; the "
                          "config then says so and value counts only their routes)")
+    ap.add_argument("--event-every", type=int, default=4,
+                    help="bracket every k-th timed launch with HIP events (kernel time; "
+                         "the events themselves cost a few us per step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-flows", action="store_true",
                     help="dfs mode: skip the materialised flow-entry rate of every host pair")
@@ -520,10 +525,15 @@ def main():
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     t_src = my.to(dev)
-    packed = args.mode == "dfs" and args.layout != "int32" and V <= 0xFFFF and \
+    port16 = args.mode == "dfs" and args.layout in ("auto", "packed") and V <= 0xFFFF and \
         csr.E > 0 and int(csr.port.min()) >= 0 and int(csr.port.max()) < 0xFFFF
-    if args.layout == "packed" and not packed:
+    if args.layout == "packed" and not port16:
         raise SystemExit("--layout packed: fabric has V > 65535 or ports >= 0xFFFF")
+    slots = args.mode == "dfs" and not port16 and args.layout in ("auto", "slots") and \
+        V < (1 << 26) and csr.max_degree() <= 63
+    if args.layout == "slots" and not slots:
+        raise SystemExit("--layout slots: fabric has a switch with more than 63 links")
+    packed = port16 or slots                  # one u32 per tree entry
     def tables():
         if packed:
             return (torch.empty((per, V), dtype=torch.int32, device=dev),)   # parent | port << 16
@@ -552,7 +562,9 @@ def main():
         tb = bufs[k]
         if ev is not None:
             ev[0].record(stream)
-        if packed:
+        if slots:
+            ctx.dfs_tables_slots_device(t_src.data_ptr(), per, tb[0].data_ptr())
+        elif packed:
             ctx.dfs_tables_packed_device(t_src.data_ptr(), per, tb[0].data_ptr())
         elif args.mode == "dfs":
             ctx.dfs_tables_device(t_src.data_ptr(), per, tb[0].data_ptr(), tb[1].data_ptr())
@@ -581,8 +593,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    every = max(1, args.event_every)
     for i in range(args.steps):
-        step(evs[i])
+        step(evs[i] if i % every == 0 else None)
     drain()
     torch.cuda.synchronize(dev)
     ctx.synchronize()          # raises if a kernel's bounded wait tripped: tables invalid
@@ -593,7 +606,8 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for i, (e0, e1) in enumerate(evs)
+                             if i % every == 0]))
 
     ms_per_step = elapsed / args.steps * 1e3
     routes = float(counts.sum()) * float(H)      # every host pair of these sources
@@ -603,12 +617,13 @@ def main():
     per_entry = (4 if packed else 8) if args.mode == "dfs" else 10
     compulsory = 4 * (V + 1) + 8 * E + per_entry * V * (hi - lo)
     traffic = None
-    layout = "packed" if packed else ("int32" if args.mode == "dfs" else "u16+int32")
+    layout = "slots" if slots else ("packed" if packed else
+                                    ("int32" if args.mode == "dfs" else "u16+int32"))
     if os.path.exists(TRAFFIC_FILE):
         try:
             tf = json.load(open(TRAFFIC_FILE))
             traffic = tf.get("%s/%s%s/N%d" % (args.fabric, args.mode,
-                                               "-packed" if packed else "", world))
+                                               "-" + layout if packed else "", world))
         except Exception:   # noqa: BLE001
             traffic = None
     out = {
@@ -656,7 +671,9 @@ def main():
         reps = max(1, min(5, args.steps))
         t0 = time.perf_counter()
         for _ in range(reps):
-            if packed:
+            if slots:
+                ctx.dfs_tables_slots(srcs)
+            elif packed:
                 ctx.dfs_tables_packed(srcs)
             else:
                 ctx.dfs_tables(srcs, with_hops=False)
@@ -664,7 +681,8 @@ def main():
         out["host_boundary"] = {
             "value": routes / dt, "unit": "routes/s", "ms_per_call": dt * 1e3,
             "note": "sdnr_dfs_tables%s with host buffers (sources H2D, tables D2H, "
-                    "synchronous), not the HBM-resident bench value" % ("_packed" if packed else "")}
+                    "synchronous), not the HBM-resident bench value" % (
+                        "_" + layout if packed else "")}
     # fat-trees only: their default routes are ~70 entries; a torus or
     # Jellyfish all-pairs fdb set (~2,400-5,600 entries per pair) is TBs
     if rank == 0 and world == 1 and args.mode == "dfs" and not args.max_sources and \

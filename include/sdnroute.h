@@ -128,6 +128,19 @@ int sdnr_dfs_tables(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc,
 int sdnr_dfs_tables_packed(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc,
                            uint32_t *tree, uint32_t flags);
 
+/* The same default-route trees for any fabric size (4 bytes per entry; the
+ * packed layout above needs V <= 65535):
+ *   tree[i*V+v] = parent | slot << 26   slot: position of v in parent's
+ *                                         ascending neighbour list (links[
+ *                                         parent] sorted by dpid, the CSR row);
+ *                                         the port is that link's src.port_no;
+ *                                         slot 63 for the root,
+ *   tree[i*V+v] = 0xFFFFFFFF            v unreachable (SDNR_TREE_NONE).
+ * The table pass stores one word per vertex and looks no port up.  Needs
+ * V < 2^26 and every switch with <= 63 links, else SDNR_ERR_INVAL. */
+int sdnr_dfs_tables_slots(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc,
+                          uint32_t *tree, uint32_t flags);
+
 /* Shortest routes, find_route(src, dst, multiple=True) -> _find_routes_bfs
  * (topology_db.py:86-122, called from :168-180), as per-destination tables:
  * for every destination dst[i] and every vertex x

@@ -596,6 +596,12 @@ static int shard_dfs_packed(sdnr_ctx *c, const int32_t *ids, int32_t n, void *co
     return sdnr_launch_dfs(c, ids, n, nullptr, nullptr, nullptr, static_cast<uint32_t *>(o[0]));
 }
 
+static int shard_dfs_slots(sdnr_ctx *c, const int32_t *ids, int32_t n, void *const o[3])
+{
+    return sdnr_launch_dfs(c, ids, n, nullptr, nullptr, nullptr, static_cast<uint32_t *>(o[0]),
+                           true);
+}
+
 static int shard_shortest(sdnr_ctx *c, const int32_t *ids, int32_t n, void *const o[3])
 {
     return sdnr_launch_shortest(c, ids, n, static_cast<uint16_t *>(o[0]),
@@ -627,6 +633,21 @@ int sdnr_dfs_tables_packed(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc, uint
     void *const out[3] = {tree, nullptr, nullptr};
     const size_t es[3] = {4, 0, 0};
     return run_sharded(ctx, src, nsrc, out, es, flags, shard_dfs_packed);
+}
+
+int sdnr_dfs_tables_slots(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc, uint32_t *tree,
+                          uint32_t flags)
+{
+    int rc = begin_call(ctx, nsrc, src, flags, "sdnr_dfs_tables_slots");
+    if (rc) return rc;
+    if (nsrc > 0 && !tree) return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_tables_slots: null table");
+    if (ctx->V > (1 << 26) - 1 || ctx->max_deg > 63)
+        return sdnr_fail(SDNR_ERR_INVAL,
+                         "sdnr_dfs_tables_slots: needs V < 2^26 and rows of <= 63 links "
+                         "(V=%d, max degree %d)", ctx->V, ctx->max_deg);
+    void *const out[3] = {tree, nullptr, nullptr};
+    const size_t es[3] = {4, 0, 0};
+    return run_sharded(ctx, src, nsrc, out, es, flags, shard_dfs_slots);
 }
 
 int sdnr_shortest_tables(sdnr_ctx *ctx, const int32_t *dst, int32_t ndst, uint16_t *dist,

@@ -112,7 +112,8 @@ int sdnr_check_watchdog(sdnr_ctx *ctx);   // after a stream sync
 // asynchronous on ctx->stream
 int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
                     int32_t *d_parent, int32_t *d_port, int32_t *d_hops,
-                    uint32_t *d_tree);        // d_tree: packed layout instead of the three
+                    uint32_t *d_tree,         // d_tree: packed layout instead of the three
+                    bool slots = false);      // d_tree as parent | slot << 26
 int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
                          uint16_t *d_dist, int32_t *d_nh, int32_t *d_nh_port);
 int sdnr_launch_apsp(sdnr_ctx *ctx, uint16_t *d_dist);

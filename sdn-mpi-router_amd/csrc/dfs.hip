@@ -1104,7 +1104,11 @@ __host__ __device__ inline size_t split_lds_words(int V, int ring, int ns, bool 
            ((3 * (size_t)ns + 3) & ~(size_t)3);
 }
 
-template <int LPR, int J, bool HOPS, int RING, int NS, int FMT, bool PACKED>
+// tree layouts of the split kernel: int32 parent/port tables, parent | port
+// << 16 (sdnr_dfs_tables_packed), parent | slot << 26 (sdnr_dfs_tables_slots)
+constexpr int kTreeInt32 = 0, kTreePort16 = 1, kTreeSlot = 2;
+
+template <int LPR, int J, bool HOPS, int RING, int NS, int FMT, int PK>
 __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
     int V, int W, const void *__restrict__ rows, const uint32_t *__restrict__ rhi,
     const int32_t *__restrict__ ell_port, const int32_t *__restrict__ src, int nsrc,
@@ -1116,6 +1120,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
     constexpr int K = R * J;
     constexpr unsigned kSpin = 1u << 22;
     constexpr unsigned kIdle = 1u << 26;
+    constexpr bool PACKED = PK != kTreeInt32;
     static_assert(K <= 64, "one stack slot per lane");
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int VW = (V + 31) >> 5;
@@ -1169,7 +1174,8 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
             for (int i = lane; i < VWp; i += SDNR_WAVE) vis[i] = 0u;
             if (lane == 0) {                       // the wave's LDS ops stay in order
                 vis[vsw(s >> 5)] = 1u << (s & 31);
-                prow[s] = PACKED ? (int32_t)((uint32_t)s | 0xFFFF0000u) : s;
+                prow[s] = PK == kTreePort16 ? (int32_t)((uint32_t)s | 0xFFFF0000u)
+                        : PK == kTreeSlot  ? (int32_t)((uint32_t)s | (63u << 26)) : s;
                 if (!PACKED) trow[s] = -1;
                 if (HOPS) hrow[s] = 0;
                 ring[0] = RE::put((uint32_t)s, 0u);
@@ -1389,29 +1395,35 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                         const uint2 r = qrec[at];
                         const int v = (int)(r.x & 0x3FFFFFFu), slot = (int)(r.x >> 26);
                         const int par = (int)r.y;
-                        const int pt = (flags & kFlagNoPort) ? slot : ell_port[(size_t)par * W + slot];
                         const size_t e = (size_t)row * V + v;
-                        if (flags & kFlagNoStore) {
-                            // diagnostic: records consumed, no table stores
-                        } else if (flags & kFlagNT) {
-                            if (PACKED) {
-                                __builtin_nontemporal_store(
-                                    (int32_t)(((uint32_t)par & 0xFFFFu) | ((uint32_t)pt << 16)),
-                                    &out_parent[e]);
-                            } else {
-                                __builtin_nontemporal_store(par, &out_parent[e]);
-                                __builtin_nontemporal_store(pt, &out_port[e]);
-                            }
-                            if (HOPS) __builtin_nontemporal_store((int)qdep[at], &out_hops[e]);
+                        if (PK == kTreeSlot) {     // no port lookup: the slot names it
+                            if (!(flags & kFlagNoStore))
+                                out_parent[e] = (int32_t)((uint32_t)par | ((uint32_t)slot << 26));
                         } else {
-                            if (PACKED) {
-                                out_parent[e] = (int32_t)(((uint32_t)par & 0xFFFFu) |
-                                                          ((uint32_t)pt << 16));
+                            const int pt = (flags & kFlagNoPort) ? slot
+                                                                 : ell_port[(size_t)par * W + slot];
+                            if (flags & kFlagNoStore) {
+                                // diagnostic: records consumed, no table stores
+                            } else if (flags & kFlagNT) {
+                                if (PACKED) {
+                                    __builtin_nontemporal_store(
+                                        (int32_t)(((uint32_t)par & 0xFFFFu) | ((uint32_t)pt << 16)),
+                                        &out_parent[e]);
+                                } else {
+                                    __builtin_nontemporal_store(par, &out_parent[e]);
+                                    __builtin_nontemporal_store(pt, &out_port[e]);
+                                }
+                                if (HOPS) __builtin_nontemporal_store((int)qdep[at], &out_hops[e]);
                             } else {
-                                out_parent[e] = par;
-                                out_port[e] = pt;
+                                if (PACKED) {
+                                    out_parent[e] = (int32_t)(((uint32_t)par & 0xFFFFu) |
+                                                              ((uint32_t)pt << 16));
+                                } else {
+                                    out_parent[e] = par;
+                                    out_port[e] = pt;
+                                }
+                                if (HOPS) out_hops[e] = (int)qdep[at];
                             }
-                            if (HOPS) out_hops[e] = (int)qdep[at];
                         }
                     }
                     consd[k] = C + n;
@@ -1753,6 +1765,33 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
 #endif
 }
 
+// slot trees from int32 ones: slot = position of v in parent's ascending CSR
+// row (binary search); the root (parent == v) gets slot 63
+__global__ __launch_bounds__(256) void dfs_slot_pack_kernel(size_t n, int V,
+                                                            const int32_t *__restrict__ parent,
+                                                            const int32_t *__restrict__ row_ptr,
+                                                            const int32_t *__restrict__ col,
+                                                            uint32_t *__restrict__ tree)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const int v = (int)(i % (size_t)V), p = parent[i];
+        uint32_t t = 0xFFFFFFFFu;
+        if (p == v) {
+            t = (uint32_t)p | (63u << 26);
+        } else if (p >= 0) {
+            int lo = row_ptr[p], hi = row_ptr[p + 1];
+            const int base = lo;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (col[mid] < v) lo = mid + 1; else hi = mid;
+            }
+            t = (uint32_t)p | ((uint32_t)(lo - base) << 26);
+        }
+        tree[i] = t;
+    }
+}
+
 // packed tables from int32 ones (strategies without a packed epilogue)
 __global__ __launch_bounds__(256) void dfs_pack_kernel(size_t n, const int32_t *__restrict__ parent,
                                                        const int32_t *__restrict__ port,
@@ -1991,13 +2030,13 @@ static bool split_ok()
 // the end event itself
 template <int NS>
 static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, int32_t *d_parent,
-                           int32_t *d_port, int32_t *d_hops, uint32_t *d_tree);
+                           int32_t *d_port, int32_t *d_hops, uint32_t *d_tree, int tree);
 
 // search waves per workgroup: 7 on sparse tori (4 workgroups of 8 waves fill
 // a CU's 32 wave slots with 28 sources), else 3 (LDS-bound: Jellyfish fits 3
 // workgroups of 3 sources); SDNROUTE_DFS_SPLIT_NS=3|7 overrides
 static int launch_split(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, int32_t *d_parent,
-                        int32_t *d_port, int32_t *d_hops, uint32_t *d_tree)
+                        int32_t *d_port, int32_t *d_hops, uint32_t *d_tree, int tree)
 {
     int ns = ctx->W <= 8 && packed_j8(ctx->V) == 1 ? 7 : 3;
     if (ctx->W > 8 && ctx->W <= 16) {
@@ -2019,16 +2058,16 @@ static int launch_split(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, int32
         if ((k == 5 || k == 11) && ctx->W > 8 && ctx->W <= 16) ns = k;   // rows of 9-16 slots
     }
     switch (ns) {
-    case 7: return launch_split_ns<7>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree);
-    case 5: return launch_split_ns<5>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree);
-    case 11: return launch_split_ns<11>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree);
-    default: return launch_split_ns<3>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree);
+    case 7: return launch_split_ns<7>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree, tree);
+    case 5: return launch_split_ns<5>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree, tree);
+    case 11: return launch_split_ns<11>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree, tree);
+    default: return launch_split_ns<3>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree, tree);
     }
 }
 
 template <int NS>
 static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, int32_t *d_parent,
-                           int32_t *d_port, int32_t *d_hops, uint32_t *d_tree)
+                           int32_t *d_port, int32_t *d_hops, uint32_t *d_tree, int tree)
 {
     const int V = ctx->V, W = ctx->W;
     const bool packed = d_tree != nullptr, hops = d_hops != nullptr;
@@ -2042,8 +2081,10 @@ static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, in
     constexpr bool kWide = NS == 5 || NS == 11;   // only for rows of 9-16 slots
     if (kWide && lpr != 16) return sdnr_fail(SDNR_ERR_INVAL, "dfs split: NS=%d needs rows of 9-16 slots", NS);
     const int fmt = ctx->ell16 && V <= 65535 ? kRow16 : (ctx->ell16 && ctx->ell_hi ? kRow17 : kRow32);
-    if (packed && fmt != kRow16)
+    if (tree == kTreePort16 && fmt != kRow16)
         return sdnr_fail(SDNR_ERR_INVAL, "dfs split: packed tables need V <= 65535");
+    if (tree == kTreeSlot && hops)
+        return sdnr_fail(SDNR_ERR_INVAL, "dfs split: slot trees carry no hop counts");
     const size_t lds = split_lds_words(V, ring, NS, hops, lpr) * 4;
     if (lds > SDNR_MAX_LDS_PER_BLOCK)
         return sdnr_fail(SDNR_ERR_INVAL, "graph too large for the LDS visited sets (V=%d)", V);
@@ -2060,10 +2101,11 @@ static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, in
     const void *rows = fmt == kRow32 ? static_cast<const void *>(ctx->ell_col)
                                      : static_cast<const void *>(ctx->ell16);
     int32_t *par = packed ? reinterpret_cast<int32_t *>(d_tree) : d_parent;
-    static const char *names[3][2] = {{"dfs_split_kernel<row32>", "dfs_split_kernel<row32>"},
-                                      {"dfs_split_kernel<row16>", "dfs_split_kernel<row16,packed>"},
-                                      {"dfs_split_kernel<row17>", "dfs_split_kernel<row17>"}};
-    ctx->last_kernel = names[fmt][packed ? 1 : 0];
+    static const char *names[3][3] = {
+        {"dfs_split_kernel<row32>", "dfs_split_kernel<row32>", "dfs_split_kernel<row32,slots>"},
+        {"dfs_split_kernel<row16>", "dfs_split_kernel<row16,packed>", "dfs_split_kernel<row16,slots>"},
+        {"dfs_split_kernel<row17>", "dfs_split_kernel<row17>", "dfs_split_kernel<row17,slots>"}};
+    ctx->last_kernel = names[fmt][tree];
 #define SDNR_SPLIT(L_, J_, R_, H_, F_, P_)                                                    \
     do {                                                                                     \
         auto k = dfs_split_kernel<L_, J_, H_, R_, NS, F_, P_>;                               \
@@ -2074,10 +2116,18 @@ static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, in
     } while (0)
 #define SDNR_SPLIT_F(L_, J_, R_, H_)                                                          \
     do {                                                                                     \
-        if (fmt == kRow16 && packed) SDNR_SPLIT(L_, J_, R_, H_, kRow16, true);               \
-        else if (fmt == kRow16) SDNR_SPLIT(L_, J_, R_, H_, kRow16, false);                   \
-        else if (fmt == kRow17) SDNR_SPLIT(L_, J_, R_, H_, kRow17, false);                   \
-        else SDNR_SPLIT(L_, J_, R_, H_, kRow32, false);                                      \
+        if constexpr (!H_) {                                                                 \
+            if (tree == kTreeSlot) {                                                         \
+                if (fmt == kRow16) SDNR_SPLIT(L_, J_, R_, H_, kRow16, kTreeSlot);            \
+                else if (fmt == kRow17) SDNR_SPLIT(L_, J_, R_, H_, kRow17, kTreeSlot);       \
+                else SDNR_SPLIT(L_, J_, R_, H_, kRow32, kTreeSlot);                          \
+                break;                                                                       \
+            }                                                                                \
+        }                                                                                    \
+        if (fmt == kRow16 && packed) SDNR_SPLIT(L_, J_, R_, H_, kRow16, kTreePort16);        \
+        else if (fmt == kRow16) SDNR_SPLIT(L_, J_, R_, H_, kRow16, kTreeInt32);              \
+        else if (fmt == kRow17) SDNR_SPLIT(L_, J_, R_, H_, kRow17, kTreeInt32);              \
+        else SDNR_SPLIT(L_, J_, R_, H_, kRow32, kTreeInt32);                                 \
     } while (0)
 #define SDNR_SPLIT_H(L_, J_, R_)                                                              \
     do {                                                                                     \
@@ -2102,7 +2152,8 @@ static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, in
 }
 
 int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
-                    int32_t *d_parent, int32_t *d_port, int32_t *d_hops, uint32_t *d_tree)
+                    int32_t *d_parent, int32_t *d_port, int32_t *d_hops, uint32_t *d_tree,
+                    bool slots)
 {
     const int V = ctx->V;
     if (nsrc == 0 || V == 0) return SDNR_OK;
@@ -2147,18 +2198,24 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
                           dfs_lds_bytes_count(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;
     const bool async_ok = count_ok && dfs_lds_bytes_async(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;
     const bool async = async_ok && (force ? !strcmp(force, "async") : small);
+    slots = slots && packed;
     if (!async && !small && ell && ctx->W <= 32 && packed_ok() && split_ok() &&
-        (!packed || (ctx->ell16 && V <= 65535)))
-        return launch_split(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree);
-    if (packed && !async) {
-        // no packed epilogue in this strategy: int32 tables into scratch, then pack
+        (!packed || slots || (ctx->ell16 && V <= 65535)))
+        return launch_split(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree,
+                            slots ? kTreeSlot : (packed ? kTreePort16 : kTreeInt32));
+    if (packed && (!async || slots)) {
+        // no such epilogue in this strategy: int32 tables into scratch, then pack
         const size_t n = (size_t)nsrc * (size_t)V;
         int rc = sdnr_reserve(&ctx->scratch2, &ctx->scratch2_bytes, 2 * n * sizeof(int32_t));
         if (rc) return rc;
         int32_t *tp = static_cast<int32_t *>(ctx->scratch2);
         if ((rc = sdnr_launch_dfs(ctx, d_src, nsrc, tp, tp + n, nullptr, nullptr))) return rc;
-        hipLaunchKernelGGL(dfs_pack_kernel, dim3(ctx->num_cus * 8), dim3(256), 0, ctx->stream, n,
-                           tp, tp + n, d_tree);
+        if (slots)
+            hipLaunchKernelGGL(dfs_slot_pack_kernel, dim3(ctx->num_cus * 8), dim3(256), 0,
+                               ctx->stream, n, V, tp, ctx->row_ptr, ctx->col, d_tree);
+        else
+            hipLaunchKernelGGL(dfs_pack_kernel, dim3(ctx->num_cus * 8), dim3(256), 0, ctx->stream,
+                               n, tp, tp + n, d_tree);
         SDNR_HIP(hipGetLastError());
         if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
         return SDNR_OK;

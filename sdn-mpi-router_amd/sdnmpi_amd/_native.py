@@ -33,7 +33,8 @@ ABI_VERSION = 1
 EXPORTED_SYMBOLS = (
     "sdnr_abi_version", "sdnr_last_error", "sdnr_device_count", "sdnr_create",
     "sdnr_create_multi", "sdnr_device_list", "sdnr_destroy", "sdnr_set_stream", "sdnr_synchronize", "sdnr_graph_upload",
-    "sdnr_graph_info", "sdnr_dfs_tables", "sdnr_dfs_tables_packed", "sdnr_shortest_tables",
+    "sdnr_graph_info", "sdnr_dfs_tables", "sdnr_dfs_tables_packed", "sdnr_dfs_tables_slots",
+    "sdnr_shortest_tables",
     "sdnr_apsp", "sdnr_route_offsets", "sdnr_route_expand", "sdnr_ecmp_counts",
     "sdnr_ecmp_routes",
     "sdnr_last_kernel_ms", "sdnr_last_kernel", "sdnr_last_launches", "sdnr_edge_ports",
@@ -75,6 +76,7 @@ def _bind(L):
                              ctypes.POINTER(i32)], c_int),
         "sdnr_dfs_tables": ([vp, vp, i32, vp, vp, vp, u32], c_int),
         "sdnr_dfs_tables_packed": ([vp, vp, i32, vp, u32], c_int),
+        "sdnr_dfs_tables_slots": ([vp, vp, i32, vp, u32], c_int),
         "sdnr_shortest_tables": ([vp, vp, i32, vp, vp, vp, u32], c_int),
         "sdnr_apsp": ([vp, vp, u32], c_int),
         "sdnr_route_offsets": ([vp, vp, i32, vp, vp, i32, vp, u32], c_int),
@@ -140,6 +142,24 @@ def unpack_tree(tree):
     port = (t >> 16).astype(np.int32)
     parent[parent == 0xFFFF] = -1
     port[port == 0xFFFF] = -1
+    return parent, port
+
+
+def unpack_slots(tree, csr):
+    """Slot tree rows (parent | slot << 26) -> (parent, port) int32 with the
+    CSR's port of each tree link; -1 for unreached vertices and the root's
+    port."""
+    t = np.asarray(tree, np.uint32)
+    none = t == TREE_NONE
+    parent = (t & 0x3FFFFFF).astype(np.int64)
+    slot = (t >> 26).astype(np.int64)
+    root = slot == 63
+    rp = np.asarray(csr.row_ptr, np.int64)
+    idx = np.where(none | root, 0, rp[np.where(none, 0, parent)] + slot)
+    port = np.asarray(csr.port, np.int32)[idx]
+    port[none | root] = -1
+    parent = parent.astype(np.int32)
+    parent[none] = -1
     return parent, port
 
 
@@ -234,6 +254,14 @@ class Context(object):
         S, V = int(srcs.shape[0]), self.V
         tree = np.empty((S, V), np.uint32)
         _check(self._lib.sdnr_dfs_tables_packed(self._h, _ptr(srcs), S, _ptr(tree), 0))
+        return tree
+
+    def dfs_tables_slots(self, srcs):
+        """Slot trees: uint32 [S, V], parent | slot << 26 (see unpack_slots)."""
+        srcs = np.ascontiguousarray(srcs, np.int32)
+        S, V = int(srcs.shape[0]), self.V
+        tree = np.empty((S, V), np.uint32)
+        _check(self._lib.sdnr_dfs_tables_slots(self._h, _ptr(srcs), S, _ptr(tree), 0))
         return tree
 
     def shortest_tables(self, dsts, with_nexthop=True):
@@ -345,6 +373,11 @@ class Context(object):
         flags = DEVICE_PTRS | (TIMING if timing else 0)
         _check(self._lib.sdnr_dfs_tables_packed(self._h, ctypes.c_void_p(src_ptr), int(nsrc),
                                                 ctypes.c_void_p(tree_ptr), flags))
+
+    def dfs_tables_slots_device(self, src_ptr, nsrc, tree_ptr, timing=False):
+        flags = DEVICE_PTRS | (TIMING if timing else 0)
+        _check(self._lib.sdnr_dfs_tables_slots(self._h, ctypes.c_void_p(src_ptr), int(nsrc),
+                                               ctypes.c_void_p(tree_ptr), flags))
 
     def shortest_tables_device(self, dst_ptr, ndst, dist_ptr, nh_ptr=0, nh_port_ptr=0,
                                timing=False):

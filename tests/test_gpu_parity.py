@@ -100,6 +100,40 @@ def test_dfs_packed_small(ctx, monkeypatch, name, strategy):
     np.testing.assert_array_equal(t, to)
 
 
+def _expected_slots(csr, po):
+    """Slot-tree words from oracle parents: parent | slot << 26, slot = the
+    child's position in the parent's ascending CSR row, 63 for the root."""
+    S, V = po.shape
+    want = np.full((S, V), 0xFFFFFFFF, np.uint64)
+    for i in range(S):
+        for v in range(V):
+            p = int(po[i, v])
+            if p < 0:
+                continue
+            if p == v:
+                want[i, v] = p | (63 << 26)
+            else:
+                row = csr.col[csr.row_ptr[p]:csr.row_ptr[p + 1]]
+                want[i, v] = p | (int(np.searchsorted(row, v)) << 26)
+    return want.astype(np.uint32)
+
+
+@pytest.mark.parametrize("strategy", ["auto", "async", "lds", "global", "global-nosplit"])
+@pytest.mark.parametrize("name", ["mock", "fat_tree_k8", "dragonfly_a4_h2_p2", "random_V40",
+                                  "jellyfish_n60_r5", "torus_5x3x2", "random_V60_dense"])
+def test_dfs_slots_small(ctx, monkeypatch, name, strategy):
+    _strategy(monkeypatch, None if strategy == "auto" else strategy)
+    csr = G.Golden(name).fabric().csr()
+    srcs = np.arange(csr.V, dtype=np.int32)
+    ctx.upload(csr)
+    tree = ctx.dfs_tables_slots(srcs)
+    po, to, _ = O.dfs_tables(csr, srcs, with_hops=False, nthreads=NTHREADS)
+    np.testing.assert_array_equal(tree, _expected_slots(csr, po))
+    p, t = _native.unpack_slots(tree, csr)
+    np.testing.assert_array_equal(p, po)
+    np.testing.assert_array_equal(t, to)
+
+
 def test_dfs_packed_fullsize_k48(ctx):
     fabric = T.fat_tree(48)
     csr = fabric.csr()
