@@ -1397,8 +1397,9 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                         const int par = (int)r.y;
                         const size_t e = (size_t)row * V + v;
                         if (PK == kTreeSlot) {     // no port lookup: the slot names it
-                            if (!(flags & kFlagNoStore))
-                                out_parent[e] = (int32_t)((uint32_t)par | ((uint32_t)slot << 26));
+                            const int32_t tv = (int32_t)((uint32_t)par | ((uint32_t)slot << 26));
+                            if (flags & kFlagNT) __builtin_nontemporal_store(tv, &out_parent[e]);
+                            else if (!(flags & kFlagNoStore)) out_parent[e] = tv;
                         } else {
                             const int pt = (flags & kFlagNoPort) ? slot
                                                                  : ell_port[(size_t)par * W + slot];
