@@ -291,8 +291,8 @@ static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp)
                            changed);
         SDNR_HIP(hipGetLastError());
         int h[2] = {0, 0};
-        SDNR_HIP(hipMemcpyAsync(h, changed, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-        SDNR_HIP(hipStreamSynchronize(ctx->stream));
+        const int rc = sdnr_fetch_ints(ctx, changed, 2, h);
+        if (rc) return rc;
         if (!h[0] || (it < 31 && (long long)h[1] < (1ll << it))) break;
     }
     return SDNR_OK;

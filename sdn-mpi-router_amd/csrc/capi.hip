@@ -64,6 +64,21 @@ int sdnr_reserve(void **buf, size_t *cur, size_t need)
     return SDNR_OK;
 }
 
+int sdnr_fetch_ints(sdnr_ctx *ctx, const int *d_src, int n, int *out)
+{
+    if (n < 1 || n > 4) return sdnr_fail(SDNR_ERR_INVAL, "sdnr_fetch_ints: %d words", n);
+    SDNR_HIP(hipMemcpyAsync(ctx->h_flag, d_src, (size_t)n * sizeof(int), hipMemcpyDeviceToHost,
+                            ctx->stream));
+    SDNR_HIP(hipEventRecord(ctx->ev_flag, ctx->stream));
+    for (;;) {
+        const hipError_t e = hipEventQuery(ctx->ev_flag);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) return sdnr_hip_fail(e, "sdnr_fetch_ints");
+    }
+    for (int i = 0; i < n; ++i) out[i] = reinterpret_cast<volatile int *>(ctx->h_flag)[i];
+    return SDNR_OK;
+}
+
 static void free_graph(sdnr_ctx *c)
 {
     int32_t **bufs[] = {&c->row_ptr, &c->col, &c->port, &c->ell_col, &c->ell_port};
@@ -144,6 +159,8 @@ int sdnr_create(int device, sdnr_ctx **out)
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_flag, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&c->h_flag), 4 * sizeof(int));
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&c->d_err), sizeof(int));
     if (e == hipSuccess) e = hipMemset(c->d_err, 0, sizeof(int));
     if (e != hipSuccess) {
@@ -211,6 +228,8 @@ int sdnr_destroy(sdnr_ctx *ctx)
     if (ctx->scratch2) (void)hipFree(ctx->scratch2);
     if (ctx->stage) (void)hipFree(ctx->stage);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
+    if (ctx->h_flag) (void)hipHostFree(ctx->h_flag);
+    if (ctx->ev_flag) (void)hipEventDestroy(ctx->ev_flag);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);

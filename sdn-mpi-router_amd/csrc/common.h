@@ -76,6 +76,8 @@ struct sdnr_ctx {
     const char *last_kernel = "";       // variant launched by the last table call
     int32_t last_launches = 0;          // main-kernel launches of the last table call
     int *d_err = nullptr;               // kernel watchdog word (0 = ok)
+    int *h_flag = nullptr;              // pinned host words for level-loop checks
+    hipEvent_t ev_flag = nullptr;       // ... and the event the host spins on
 
     // multi-device context (sdnr_create_multi): this context is shard 0 on
     // the primary device; peers[k] own shard k+1 (own device, stream, graph
@@ -101,6 +103,10 @@ int sdnr_fail(int code, const char *fmt, ...);
 int sdnr_hip_fail(hipError_t e, const char *what);
 int sdnr_reserve(void **buf, size_t *cur, size_t need);
 int sdnr_check_watchdog(sdnr_ctx *ctx);   // after a stream sync
+// copy n (<= 4) ints from the device into out and wait for them with a
+// busy spin on an event: a level loop's termination check costs a few
+// microseconds instead of a blocking stream synchronize's wake-up
+int sdnr_fetch_ints(sdnr_ctx *ctx, const int *d_src, int n, int *out);
 
 #define SDNR_HIP(call)                                           \
     do {                                                         \

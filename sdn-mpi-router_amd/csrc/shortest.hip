@@ -866,21 +866,14 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
             // the first chunk checks every kGroup levels; the next ones queue
             // as many levels as it needed before their first check
             if ((lvl > guess && (lvl - guess) % kGroup == 0) || lvl == guess || lvl == 255) {
-                SDNR_HIP(hipMemcpyAsync(&h_changed, changed + lvl, sizeof(int),
-                                        hipMemcpyDeviceToHost, ctx->stream));
-                SDNR_HIP(hipStreamSynchronize(ctx->stream));
+                if ((rc = sdnr_fetch_ints(ctx, changed + lvl, 1, &h_changed))) return rc;
             }
         }
         if (h_changed) return 1;                 // deeper than 255 levels
-        // levels that reached something: the queued ones after the last
-        // change returned at once
-        int hc[256];
-        SDNR_HIP(hipMemcpyAsync(hc, changed, sizeof hc, hipMemcpyDeviceToHost, ctx->stream));
-        SDNR_HIP(hipStreamSynchronize(ctx->stream));
-        lvl = 1;
-        while (lvl < 256 && hc[lvl]) ++lvl;
-        levels += lvl;
-        guess = lvl + 1 < 255 ? lvl + 1 : 0;
+        // lvl - 1 levels were queued; those after the last change returned
+        // at once
+        levels += lvl - 1;
+        guess = lvl < 255 ? lvl : 0;
         if (const char *f = getenv("SDNROUTE_PLANE_GUESS"))   // 0: check every kGroup levels
             if (!strcmp(f, "0")) guess = 0;
         uint16_t *dist = d_dist + (size_t)c0 * 64 * V;
@@ -1058,9 +1051,8 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
                                0, ctx->stream, V, ctx->W, ctx->row_ptr, ctx->col, ctx->ell_col,
                                ndst, lvl, front, next, vis, d_dist, changed);
             SDNR_HIP(hipGetLastError());
-            SDNR_HIP(hipMemcpyAsync(&h_changed, changed, sizeof(int), hipMemcpyDeviceToHost,
-                                    ctx->stream));
-            SDNR_HIP(hipStreamSynchronize(ctx->stream));
+            int rc2 = sdnr_fetch_ints(ctx, changed, 1, &h_changed);
+            if (rc2) return rc2;
             uint64_t *t = front;
             front = next;
             next = t;
