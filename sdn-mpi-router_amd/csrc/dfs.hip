@@ -1568,35 +1568,42 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             SDNR_STAMP(st_t0);
             st_tc = st_t0;
 #endif
+            int nu = -1;        // next candidate found among the newest children
             for (;;) {
-                uint64_t m = 0;
-                int e = V;
-                while (sp > 0) {
+                int u;
+                if (nu >= 0) {
+                    u = nu;
+                    nu = -1;
+                } else {
+                    uint64_t m = 0;
+                    int e = V;
+                    while (sp > 0) {
 #ifdef SDNR_STAMPS
-                    st_skip++;
+                        st_skip++;
 #endif
-                    const int kk = sp < 64 ? sp : 64;
-                    const int at = sp - 1 - lane;
-                    e = stk[at < 0 ? 0 : at];
-                    e = lane < kk ? e : V;
-                    const uint32_t c = __hip_atomic_load(&cnt[swz(e)], __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
-                    m = __ballot(c != 0u);
-                    if (m) break;
-                    sp -= kk;
+                        const int kk = sp < 64 ? sp : 64;
+                        const int at = sp - 1 - lane;
+                        e = stk[at < 0 ? 0 : at];
+                        e = lane < kk ? e : V;
+                        const uint32_t c = __hip_atomic_load(&cnt[swz(e)], __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+                        m = __ballot(c != 0u);
+                        if (m) break;
+                        sp -= kk;
+                    }
+                    // children of the last push not yet announced (the push
+                    // block announces its own; kept for the first pops)
+                    if (pub != pubd) {
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                        if (lane == 0) __hip_atomic_store(&ctl[0], pub, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+                        pubd = pub;
+                    }
+                    if (!m) break;
+                    const int first = __ffsll((unsigned long long)m) - 1;
+                    u = read_lane(e, first);
+                    sp -= first + 1;
                 }
-                // publish the previous push's children now: the skip's LDS
-                // reads have waited for those writes, so the release is free
-                if (pub != pubd) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    if (lane == 0) __hip_atomic_store(&ctl[0], pub, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-                    pubd = pub;
-                }
-                if (!m) break;
-                const int first = __ffsll((unsigned long long)m) - 1;
-                const int u = read_lane(e, first);
-                sp -= first + 1;
 #ifdef SDNR_STAMPS
                 unsigned long long ta, tb;
                 SDNR_STAMP(ta);
@@ -1646,15 +1653,35 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
 #endif
                     __builtin_amdgcn_s_sleep(1);
                 }
+                uint32_t cc = 0u;
                 if (fresh) {
                     atomicOr(&vis[x >> 5], 1u << (x & 31));
                     ps[swz(x)] = (uint32_t)u | ((uint32_t)lane << 16);
                     if (HOPS) dep[x] = (uint16_t)(du + 1);
                     stk[sp + rank] = (uint16_t)x;
                     ring[(pub + rank) & (RING - 1)] = (uint16_t)x;
+                    // children-first: the new stack top is these children
+                    // (highest id on top); their counts are read while the
+                    // prefetched rows are still in flight
+                    cc = __hip_atomic_load(&cnt[swz(x)], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
+                const uint64_t mc = __ballot(cc != 0u);
                 pub += c;
-                sp += c;
+                // announce the children: the count gather above waited for
+                // the ring writes (LDS ops complete in order), so an LDS-only
+                // release suffices and does not wait for the row prefetches
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                if (lane == 0) __hip_atomic_store(&ctl[0], pub, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+                pubd = pub;
+                if (mc) {
+                    // children above the highest one with a count are leaves
+                    // (counts are never low): popped; it is the next candidate
+                    const int hl = highest_lane(mc);
+                    nu = read_lane(x, hl);
+                    sp += read_lane(rank, hl);
+                }
 #ifdef SDNR_STAMPS
                 SDNR_STAMP(st_tc);
                 st_pushc += st_tc - tb;
