@@ -1560,7 +1560,13 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             int pub = 1, pubd = 1, sp = 1, lo = 0;       // published / announced
-            int pu0 = -1, pu1 = -1, xpre0 = V, xpre1 = V;   // rows of the two largest children
+            constexpr int NPF = 1;        // rows of the NPF largest children in flight
+            int pu[NPF], xp[NPF];
+#pragma unroll
+            for (int k = 0; k < NPF; ++k) {
+                pu[k] = -1;
+                xp[k] = V;
+            }
 #ifdef SDNR_STAMPS
             unsigned long long st_t0, st_t1, st_row = 0, st_cand = 0, st_false = 0, st_bp = 0,
                                                st_miss = 0, st_skip = 0, st_tc = 0, st_skipc = 0,
@@ -1608,10 +1614,18 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                 unsigned long long ta, tb;
                 SDNR_STAMP(ta);
                 st_skipc += ta - st_tc;
-                if (u != pu0 && u != pu1) st_miss++;
+                {
+                    bool hit = false;
+#pragma unroll
+                    for (int k = 0; k < NPF; ++k) hit |= u == pu[k];
+                    if (!hit) st_miss++;
+                }
 #endif
-                const int x = (u == pu0) ? xpre0 : (u == pu1) ? xpre1
-                                                              : (int)adj[(size_t)u * 64 + lane];
+                int x = -1;
+#pragma unroll
+                for (int k = 0; k < NPF; ++k)
+                    if (x < 0 && u == pu[k]) x = xp[k];
+                if (x < 0) x = (int)adj[(size_t)u * 64 + lane];
                 const uint32_t wv = vis[x >> 5];
                 const bool fresh = ((wv >> (x & 31)) & 1u) == 0u;
                 const uint64_t mm = __ballot(fresh);
@@ -1628,11 +1642,20 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                 const int c = __popcll(mm);
                 const int rank = lanes_below(mm);
                 // the next candidates are most likely the newest children
-                pu0 = read_lane(x, highest_lane(mm));
-                const uint64_t rest = mm & ~(1ull << highest_lane(mm));
-                pu1 = rest ? read_lane(x, highest_lane(rest)) : -1;
-                xpre0 = adj[(size_t)pu0 * 64 + lane];
-                xpre1 = adj[(size_t)(rest ? pu1 : V) * 64 + lane];
+                {
+                    uint64_t rest = mm;
+#pragma unroll
+                    for (int k = 0; k < NPF; ++k) {
+                        if (rest) {
+                            const int h = highest_lane(rest);
+                            rest &= ~(1ull << h);
+                            pu[k] = read_lane(x, h);
+                            xp[k] = adj[(size_t)pu[k] * 64 + lane];
+                        } else {
+                            pu[k] = -1;
+                        }
+                    }
+                }
                 int du = 0;
                 if (HOPS) du = uniform((int)dep[u]);
                 // back-pressure: ring slots below every worker's progress are
