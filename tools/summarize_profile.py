@@ -31,8 +31,10 @@ def main(src, out):
             per[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
             meta[k] = {x: r[x] for x in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size",
                                         "VGPR_Count", "SGPR_Count", "Scratch_Size")}
+    # dispatches: the fewest values of any counter (a counter listed in two
+    # passes -- SQ_INSTS_LDS -- has one value per dispatch per pass)
     pmc = {k: {"meta": meta[k], "counters": {c: sum(v) / len(v) for c, v in cs.items()},
-               "dispatches": max(len(v) for v in cs.values())}
+               "dispatches": min(len(v) for v in cs.values())}
            for k, cs in per.items()}
     json.dump(pmc, open(out + "_pmc.json", "w"), indent=1, sort_keys=True)
     lines = ["# rocprofv3 summary: %s" % os.path.basename(out), ""]
