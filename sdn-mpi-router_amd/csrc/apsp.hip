@@ -268,9 +268,107 @@ __global__ __launch_bounds__(256) void minplus_square_kernel(int Vp, uint16_t *_
     if (lane_id() == 0) atomicMax(reinterpret_cast<unsigned *>(changed) + 1, mx);
 }
 
+
+// Same pass on 64 x 64 output tiles, 128 threads (each 4 rows x 8 columns):
+// 4x the workgroups of the 128 x 128 tiling, so they spread evenly over the
+// CUs (k=48: 2,025 two-wave groups, <= 8 per CU, vs 529 four-wave groups of
+// which 17 CUs got a third -- the last CUs set the pass time), and V needs
+// padding only to a multiple of 64 (k=48: none).  Per k step a thread reads
+// 4 A values (ds_read_b64) and 8 B values (ds_read_b128): 4 splats, 16 adds,
+// 16 mins for 32 outputs -- the 128-tile kernel's VALU per output.
+constexpr int MT64 = 64;
+constexpr int LDA64 = MT64 + 8;
+
+__global__ __launch_bounds__(128) void minplus_square64_kernel(int Vp, uint16_t *__restrict__ D,
+                                                               int *__restrict__ changed)
+{
+    __shared__ __attribute__((aligned(16))) uint16_t As[KS][LDA64];   // As[k][i] = D[i0+i][k0+k]
+    __shared__ __attribute__((aligned(16))) uint16_t Bs[KS][LDA64];   // Bs[k][j] = D[k0+k][j0+j]
+    const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
+    const int i0 = blockIdx.y * MT64, j0 = blockIdx.x * MT64;
+    u16x2 acc[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(D + (size_t)(i0 + ty * 4 + r) * Vp + j0 + tx * 8);
+        acc[r][0] = as_pk(v.x);
+        acc[r][1] = as_pk(v.y);
+        acc[r][2] = as_pk(v.z);
+        acc[r][3] = as_pk(v.w);
+    }
+    uint4 ra0, ra1, rb0, rb1;
+    auto load_slice = [&](int k0) {
+        const int L0 = threadIdx.x, L1 = threadIdx.x + 128;
+        ra0 = *reinterpret_cast<const uint4 *>(D + (size_t)(i0 + (L0 >> 2)) * Vp + k0 + (L0 & 3) * 8);
+        ra1 = *reinterpret_cast<const uint4 *>(D + (size_t)(i0 + (L1 >> 2)) * Vp + k0 + (L1 & 3) * 8);
+        rb0 = *reinterpret_cast<const uint4 *>(D + (size_t)(k0 + (L0 >> 3)) * Vp + j0 + (L0 & 7) * 8);
+        rb1 = *reinterpret_cast<const uint4 *>(D + (size_t)(k0 + (L1 >> 3)) * Vp + j0 + (L1 & 7) * 8);
+    };
+    auto store_a = [&](int L, const uint4 &v) {         // transpose into As[k][i]
+        const int i = L >> 2, kq = (L & 3) * 8;
+        As[kq + 0][i] = (uint16_t)(v.x & 0xFFFFu);
+        As[kq + 1][i] = (uint16_t)(v.x >> 16);
+        As[kq + 2][i] = (uint16_t)(v.y & 0xFFFFu);
+        As[kq + 3][i] = (uint16_t)(v.y >> 16);
+        As[kq + 4][i] = (uint16_t)(v.z & 0xFFFFu);
+        As[kq + 5][i] = (uint16_t)(v.z >> 16);
+        As[kq + 6][i] = (uint16_t)(v.w & 0xFFFFu);
+        As[kq + 7][i] = (uint16_t)(v.w >> 16);
+    };
+    load_slice(0);
+    for (int k0 = 0; k0 < Vp; k0 += KS) {
+        store_a(threadIdx.x, ra0);
+        store_a(threadIdx.x + 128, ra1);
+        *reinterpret_cast<uint4 *>(&Bs[threadIdx.x >> 3][(threadIdx.x & 7) * 8]) = rb0;
+        *reinterpret_cast<uint4 *>(&Bs[(threadIdx.x + 128) >> 3][(threadIdx.x & 7) * 8]) = rb1;
+        __syncthreads();
+        if (k0 + KS < Vp) load_slice(k0 + KS);
+#pragma unroll 8
+        for (int k = 0; k < KS; ++k) {
+            const uint2 av = *reinterpret_cast<const uint2 *>(&As[k][ty * 4]);
+            const uint4 bv = *reinterpret_cast<const uint4 *>(&Bs[k][tx * 8]);
+            const u16x2 b[4] = {as_pk(bv.x), as_pk(bv.y), as_pk(bv.z), as_pk(bv.w)};
+            const uint32_t aw[2] = {av.x, av.y};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const u16x2 as = as_pk(__builtin_amdgcn_perm(aw[r >> 1], aw[r >> 1],
+                                                             (r & 1) ? 0x03020302u : 0x01000100u));
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    acc[r][c] = __builtin_elementwise_min(acc[r][c],
+                                                          __builtin_elementwise_add_sat(as, b[c]));
+            }
+        }
+        __syncthreads();
+    }
+    bool any = false;
+    uint32_t mx = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        uint16_t *p = D + (size_t)(i0 + ty * 4 + r) * Vp + j0 + tx * 8;
+        const uint4 o = *reinterpret_cast<const uint4 *>(p);
+        uint4 v;
+        v.x = as_u32(acc[r][0]);
+        v.y = as_u32(acc[r][1]);
+        v.z = as_u32(acc[r][2]);
+        v.w = as_u32(acc[r][3]);
+        any |= (v.x != o.x) | (v.y != o.y) | (v.z != o.z) | (v.w != o.w);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t w = as_u32(acc[r][c]);
+            const uint32_t lo = w & 0xFFFFu, hi = w >> 16;
+            mx = max(mx, lo == 0xFFFFu ? 0u : lo);
+            mx = max(mx, hi == 0xFFFFu ? 0u : hi);
+        }
+        *reinterpret_cast<uint4 *>(p) = v;
+    }
+    if (__ballot(any) && lane_id() == 0) atomicOr(changed, 1);
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    if (lane_id() == 0) atomicMax(reinterpret_cast<unsigned *>(changed) + 1, mx);
+}
+
 }  // namespace
 
-static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp)
+static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp, int mt)
 {
     int rc = sdnr_reserve(&ctx->scratch2, &ctx->scratch2_bytes, 256);
     if (rc) return rc;
@@ -282,13 +380,17 @@ static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp)
     // stop when a pass changes nothing, or when after s squarings (exact for
     // every distance <= 2^s) the largest finite distance M is < 2^s: no pair
     // is at distance M + 1 <= 2^s, so none is farther
-    const int nt = Vp / MT;
+    const int nt = Vp / mt;
     ctx->last_launches = 0;
     for (int it = 1; it <= 40; ++it) {         // 2^40 >> any hop distance
         ctx->last_launches = it;
         SDNR_HIP(hipMemsetAsync(changed, 0, 2 * sizeof(int), ctx->stream));
-        hipLaunchKernelGGL(minplus_square_kernel, dim3(nt, nt), dim3(256), 0, ctx->stream, Vp, D,
-                           changed);
+        if (mt == MT64)
+            hipLaunchKernelGGL(minplus_square64_kernel, dim3(nt, nt), dim3(128), 0, ctx->stream,
+                               Vp, D, changed);
+        else
+            hipLaunchKernelGGL(minplus_square_kernel, dim3(nt, nt), dim3(256), 0, ctx->stream, Vp,
+                               D, changed);
         SDNR_HIP(hipGetLastError());
         int h[2] = {0, 0};
         const int rc = sdnr_fetch_ints(ctx, changed, 2, h);
@@ -303,11 +405,13 @@ int sdnr_launch_apsp(sdnr_ctx *ctx, uint16_t *d_dist)
     const int V = ctx->V;
     if (V == 0) return SDNR_OK;
     if (V > 16384) return sdnr_fail(SDNR_ERR_INVAL, "apsp: V=%d > 16384", V);
-    // SDNROUTE_APSP=fw selects the blocked Floyd-Warshall (A/B, tests)
+    // SDNROUTE_APSP=fw selects the blocked Floyd-Warshall, =sq128 the
+    // 128 x 128-tile squaring (A/B, tests); default: 64 x 64-tile squaring
     const char *f = getenv("SDNROUTE_APSP");
     const bool fw = f && !strcmp(f, "fw");
-    const int nb = (V + (fw ? T : MT) - 1) / (fw ? T : MT);
-    const int Vp = nb * (fw ? T : MT);
+    const int mt = f && !strcmp(f, "sq128") ? MT : MT64;
+    const int nb = (V + (fw ? T : mt) - 1) / (fw ? T : mt);
+    const int Vp = nb * (fw ? T : mt);
     const size_t bytes = (size_t)Vp * Vp * sizeof(uint16_t);
     uint16_t *D = d_dist;
     if (Vp != V) {
@@ -316,9 +420,9 @@ int sdnr_launch_apsp(sdnr_ctx *ctx, uint16_t *d_dist)
         D = static_cast<uint16_t *>(ctx->scratch);
     }
     if (!fw) {
-        ctx->last_kernel = "minplus_square_kernel";
+        ctx->last_kernel = mt == MT64 ? "minplus_square64_kernel" : "minplus_square_kernel";
         if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
-        int rc = launch_apsp_squaring(ctx, D, V, Vp);
+        int rc = launch_apsp_squaring(ctx, D, V, Vp, mt);
         if (rc) return rc;
         if (D != d_dist)
             SDNR_HIP(hipMemcpy2DAsync(d_dist, (size_t)V * 2, D, (size_t)Vp * 2, (size_t)V * 2, V,
