@@ -471,7 +471,8 @@ def main_apsp(args, world, rank, local, dev):
         "data": "synthetic (canonical fabric)",
         "config": {"workload": "%s APSP (V=%d)" % (args.fabric, V), "fabric": args.fabric, "V": V},
         "roofline": {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "Tops/s",
-                     "frac": achieved / peak, "traffic": None, "kernel": ctx.last_kernel(),
+                     "frac": achieved / peak, "traffic": _traffic("%s/apsp/N1" % args.fabric),
+                     "kernel": ctx.last_kernel(),
                      "kernel_ms": kern_ms, "ops_per_launch": ops, "passes": passes,
                      "padded_ops_per_launch": passes * 2.0 * float(Vp) ** 3},
     }

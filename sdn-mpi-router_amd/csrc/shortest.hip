@@ -669,16 +669,18 @@ __global__ __launch_bounds__(NW * 64) void bfs_dest_lanes_kernel(
 // batches so the scratch stays bounded.
 // ---------------------------------------------------------------------------
 constexpr int kPlVis = 0, kPlFront = 1, kPlNext = 2, kPlDist = 3, kPlSlot = 11;
-constexpr int kPlanes = 16;                    // vis, front, next, 8 level, 5 slot
+// planes per batch: vis, front, next, 8 level, SB slot planes (SB =
+// ceil(log2 W)); 16 (a 4 MiB batch stride on the torus) up to SB = 5
+__host__ __device__ constexpr int plane_count(int sb) { return sb <= 5 ? 16 : kPlSlot + sb; }
 
 __global__ __launch_bounds__(256) void msbfs_plane_seed_kernel(
-    int V, const int32_t *__restrict__ dst, int ndst, uint64_t *__restrict__ pl)
+    int V, const int32_t *__restrict__ dst, int ndst, uint64_t *__restrict__ pl, int npl)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= ndst) return;
     const int d = dst[i];
     if (d < 0 || d >= V) return;
-    uint64_t *b = pl + (size_t)(i >> 6) * kPlanes * V;
+    uint64_t *b = pl + (size_t)(i >> 6) * npl * V;
     atomicOr((unsigned long long *)&b[(size_t)kPlVis * V + d], 1ull << (i & 63));
     atomicOr((unsigned long long *)&b[(size_t)kPlFront * V + d], 1ull << (i & 63));
 }
@@ -695,7 +697,7 @@ __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
     if (lvl > 1 && __hip_atomic_load(&changed[lvl - 1], __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT) == 0) return;
     if (x >= V) return;
-    uint64_t *b = pl + (size_t)batch * kPlanes * V;
+    uint64_t *b = pl + (size_t)batch * plane_count(SB) * V;
     const uint64_t *front = b + (size_t)(flip ? kPlNext : kPlFront) * V;
     uint64_t *next = b + (size_t)(flip ? kPlFront : kPlNext) * V;
     const int nb = min(64, ndst - batch * 64);
@@ -770,7 +772,7 @@ __global__ __launch_bounds__(256) void msbfs_plane_tables_kernel(
         __syncthreads();
     }
     if (x >= V) return;
-    const uint64_t *b = pl + (size_t)batch * kPlanes * V;
+    const uint64_t *b = pl + (size_t)batch * plane_count(SB) * V;
     const uint64_t vx = b[(size_t)kPlVis * V + x];
     uint64_t d[8], s[SB];
 #pragma unroll
@@ -817,9 +819,9 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
                         int32_t *d_nh, int32_t *d_nh_port)
 {
     const int V = ctx->V, W = ctx->W;
-    const int sb = W <= 8 ? 3 : W <= 16 ? 4 : 5;
+    const int sb = W <= 8 ? 3 : W <= 16 ? 4 : W <= 32 ? 5 : 6;
     const int nbatch = (ndst + 63) / 64;
-    const size_t per_batch = (size_t)kPlanes * V * sizeof(uint64_t);
+    const size_t per_batch = (size_t)plane_count(sb) * V * sizeof(uint64_t);
     // batches per chunk: the planes one level sweeps stay inside the 256 MiB
     // Infinity Cache (measured: torus 32^3 14.9 -> 12.8 ms with 64 batches of
     // 4 MiB instead of all 512 at once; the 100k Jellyfish 127 -> 119 ms)
@@ -830,6 +832,9 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
     }
     if (cb < 1) cb = 1;
     if (cb > nbatch) cb = nbatch;
+    // equal chunks: a short last chunk costs a whole level sequence
+    const int nchunk = (nbatch + cb - 1) / cb;
+    cb = (nbatch + nchunk - 1) / nchunk;
     int rc = sdnr_reserve(&ctx->scratch, &ctx->scratch_bytes, (size_t)cb * per_batch + 1024);
     if (rc) return rc;
     uint64_t *pl = static_cast<uint64_t *>(ctx->scratch);
@@ -843,7 +848,7 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
         const int nd = ndst - c0 * 64 < nbc * 64 ? ndst - c0 * 64 : nbc * 64;
         SDNR_HIP(hipMemsetAsync(pl, 0, (size_t)nbc * per_batch, ctx->stream));
         hipLaunchKernelGGL(msbfs_plane_seed_kernel, dim3((nd + 255) / 256), dim3(256), 0,
-                           ctx->stream, V, d_dst + (size_t)c0 * 64, nd, pl);
+                           ctx->stream, V, d_dst + (size_t)c0 * 64, nd, pl, plane_count(sb));
         SDNR_HIP(hipGetLastError());
         // levels go out in groups of kGroup with one host check per group
         constexpr int kGroup = 8;
@@ -858,8 +863,12 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
                 hipLaunchKernelGGL(msbfs_plane_level_kernel<4>, dim3(gx, nbc), dim3(256), 0,
                                    ctx->stream, V, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
                                    changed);
-            else
+            else if (sb == 5)
                 hipLaunchKernelGGL(msbfs_plane_level_kernel<5>, dim3(gx, nbc), dim3(256), 0,
+                                   ctx->stream, V, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
+                                   changed);
+            else
+                hipLaunchKernelGGL(msbfs_plane_level_kernel<6>, dim3(gx, nbc), dim3(256), 0,
                                    ctx->stream, V, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
                                    changed);
             SDNR_HIP(hipGetLastError());
@@ -888,10 +897,16 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
             hipLaunchKernelGGL(msbfs_plane_tables_kernel<4>, dim3(gx, nbc), dim3(256), tl,
                                ctx->stream, V, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
                                nhp);
-        else
+        else if (sb == 5)
             hipLaunchKernelGGL(msbfs_plane_tables_kernel<5>, dim3(gx, nbc), dim3(256), tl,
                                ctx->stream, V, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
                                nhp);
+        else {
+            sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<6>), tl);
+            hipLaunchKernelGGL(msbfs_plane_tables_kernel<6>, dim3(gx, nbc), dim3(256), tl,
+                               ctx->stream, V, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
+                               nhp);
+        }
         SDNR_HIP(hipGetLastError());
     }
     ctx->last_launches = levels;
@@ -912,10 +927,13 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
                          dlds <= 64 * 1024;
     const char *force = sp_strategy();
     // the bit-plane BFS wins wherever its rows fit and the batch is not tiny
-    // (dragonfly all-pairs 0.226 -> 0.197 ms, torus 32^3 22.6 -> 16.1 ms; a
-    // 32-destination fat-tree k=8 batch is dominated by its per-level syncs);
+    // (dragonfly all-pairs 0.226 -> 0.197 ms, torus 32^3 22.6 -> 16.1 ms, k=48
+    // 0.193 -> 0.127 ms; a 32-destination fat-tree k=8 batch is dominated by
+    // its per-level syncs);
     // SDNROUTE_SP_STRATEGY=plane|lanes|msbfs forces a kernel family
-    const bool plane_ok = ctx->W > 0 && ctx->W <= 32;
+    // rows of up to 64 slots: k=48 fat-tree (48 slots, 6 slot planes) 0.193 ->
+    // 0.127 ms over bfs_dest_kernel, bit-exact
+    const bool plane_ok = ctx->W > 0 && ctx->W <= 64;
     const bool plane_big = (size_t)ndst * (size_t)V >= ((size_t)1 << 21);
     if (plane_ok && (!strcmp(force, "plane") || (!*force && plane_big))) {
         const int rc = launch_plane(ctx, d_dst, ndst, d_dist, d_nh, d_nh_port);

@@ -276,8 +276,10 @@ def test_shortest_matches_reference_multiple(ctx, name):
             assert [int(csr.dpids[x]) for x in q] == [x for x, _ in w]
 
 
-@pytest.mark.parametrize("strategy", ["auto", "msbfs"])
+@pytest.mark.parametrize("strategy", ["auto", "dest", "msbfs"])
 def test_shortest_fullsize_fat_tree(ctx, monkeypatch, strategy):
+    """k=48: rows of 48 slots -- the bit-plane BFS with 6 slot planes (auto),
+    the per-destination BFS and the level + next-hop kernels."""
     if strategy != "auto":
         monkeypatch.setenv("SDNROUTE_SP_STRATEGY", strategy)
     fabric = T.fat_tree(48)
@@ -285,8 +287,9 @@ def test_shortest_fullsize_fat_tree(ctx, monkeypatch, strategy):
     dsts = np.unique(fabric.host_table()[0]).astype(np.int32)
     ctx.upload(csr)
     dist, nh, nhp = ctx.shortest_tables(dsts)
-    if strategy == "auto":
-        assert ctx.last_kernel().startswith("bfs_dest_kernel")
+    if strategy != "msbfs":
+        assert ctx.last_kernel().startswith({"auto": "msbfs_plane_level_kernel",
+                                             "dest": "bfs_dest_kernel"}[strategy])
     do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
     np.testing.assert_array_equal(dist, do)
     np.testing.assert_array_equal(nh, nho)
