@@ -47,7 +47,10 @@ def all_gather_rows(local, group=None):
     out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]),
                       dtype=local.dtype, device=local.device)
     if dist.get_backend(group) == "nccl":
-        dist.all_gather_into_tensor(out, local.contiguous(), group=group)
+        src, dst = local.contiguous(), out
+        if src.dtype == torch.int16:         # RCCL has no 16-bit integers: move bytes
+            src, dst = src.view(torch.uint8), out.view(torch.uint8)
+        dist.all_gather_into_tensor(dst, src, group=group)
     else:   # gloo has no all_gather_into_tensor for every dtype
         parts = list(out.chunk(world, 0))
         dist.all_gather(parts, local.contiguous(), group=group)
@@ -61,7 +64,10 @@ def all_gather_rows_async(local, out, group=None):
     the next kernel launched on the current stream overlaps it; ``wait()``
     before ``local`` or ``out`` is reused."""
     if dist.get_backend(group) == "nccl":
-        return dist.all_gather_into_tensor(out, local.contiguous(), group=group, async_op=True)
+        src = local.contiguous()
+        if src.dtype == torch.int16:         # RCCL has no 16-bit integers: move bytes
+            src, out = src.view(torch.uint8), out.view(torch.uint8)
+        return dist.all_gather_into_tensor(out, src, group=group, async_op=True)
     if local.is_cuda:        # gloo with device tensors (rehearsal): through host memory
         host = torch.empty(out.shape, dtype=out.dtype)
         src = local.contiguous().cpu()

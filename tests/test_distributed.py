@@ -124,3 +124,39 @@ def test_sharded_topologydb_route_tables(world, fabric):
         p.join(timeout=120)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=10) is True
+
+
+def _rccl_worker(port, q):
+    """One-rank RCCL process group on cuda:0: the table dtypes (int32 packed
+    trees, int16 distances) through the bench's all-gather helpers."""
+    try:
+        import sys
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        sys.path[:0] = [os.path.join(root, "sdn-mpi-router_amd")]
+        from sdnmpi_amd import distributed as D
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1,
+                                device_id=torch.device("cuda", 0))
+        ok = []
+        for dt in (torch.int32, torch.int16):
+            loc = torch.arange(6 * 10, dtype=torch.int32, device="cuda").view(6, 10).to(dt) - 7
+            out = torch.empty_like(loc)
+            D.all_gather_rows_async(loc, out).wait()
+            torch.cuda.synchronize()
+            ok.append(bool(torch.equal(out, loc)))
+        dist.destroy_process_group()
+        q.put(ok)
+    except Exception as e:   # noqa: BLE001 -- reported to the parent
+        q.put(repr(e))
+
+
+@pytest.mark.gpu
+def test_rccl_all_gather_table_dtypes():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=240)
+    p.join(60)
+    assert res == [True, True], res
