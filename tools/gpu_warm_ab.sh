@@ -1,6 +1,7 @@
 #!/bin/bash
-# A/B of the async DFS kernel's L2 warm-up (SDNROUTE_DFS_FLAGS=32 disables it):
-# kernel time at 1, 144 (one GPU's share at N=8) and all sources, k=48 and dragonfly.
+# Async DFS kernel time at 1, 144 (one GPU's share at N=8) and all sources,
+# k=48 and dragonfly, twice per SDNROUTE_DFS_FLAGS value (first used for the
+# L2 warm-up A/B, flag 32, since removed; the flags are diagnostics).
 OUT=${1:-gpurun_out/warm}
 mkdir -p "$OUT"
 for fl in 32 0 32 0; do
