@@ -2027,13 +2027,17 @@ extern "C" int sdnr_debug_stamps(unsigned long long *out16)
 #endif
 
 // waves per source of the asynchronous kernel: SDNROUTE_DFS_ASYNC_WAVES=2|3|4
-static int dfs_async_waves()
+// waves per source of the async kernel: 1 search + decrement workers, whose
+// work per child is its in-degree -- 3 workers for rows of 33-64 neighbours
+// (k=48: 0.116 ms vs 0.138 with 2), 2 for rows of <= 32 (dragonfly, 23
+// neighbours: 0.289 vs 0.300 ms with 3); SDNROUTE_DFS_ASYNC_WAVES=2..6
+static int dfs_async_waves(const sdnr_ctx *ctx)
 {
     if (const char *f = getenv("SDNROUTE_DFS_ASYNC_WAVES")) {
         const int k = atoi(f);
         if (k >= 2 && k <= 6) return k;
     }
-    return 4;
+    return ctx->max_deg <= 32 ? 3 : 4;
 }
 
 // waves per source of the counted-pop kernel: SDNROUTE_DFS_COUNT_WAVES=2|4|6
@@ -2287,7 +2291,7 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         if (cpc < 1) cpc = 1;
         int cgrid = (int)((size_t)ctx->num_cus * cpc);
         if (cgrid > nsrc) cgrid = nsrc;
-        const int nw = dfs_async_waves();
+        const int nw = dfs_async_waves(ctx);
         // the search wave issues at raised priority over the decrement
         // workers (dragonfly 0.316 -> 0.300 ms, k=48 unchanged)
         static const char *names[] = {"", "", "dfs_async_kernel<2>", "dfs_async_kernel<3>",

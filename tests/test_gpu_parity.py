@@ -145,7 +145,7 @@ def test_dfs_packed_fullsize_k48(ctx):
     np.testing.assert_array_equal(tree, _pack(po, to))
 
 
-@pytest.mark.parametrize("waves", [2, 3, 5, 6])
+@pytest.mark.parametrize("waves", [2, 3, 4, 5, 6])
 @pytest.mark.parametrize("name", ["fat_tree_k8", "jellyfish_n60_r5", "torus_5x3x2"])
 def test_dfs_packed_async_waves(ctx, monkeypatch, name, waves):
     _strategy(monkeypatch, "async")
