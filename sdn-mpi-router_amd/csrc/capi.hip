@@ -87,6 +87,9 @@ static void free_graph(sdnr_ctx *c)
         *b = nullptr;
     }
     if (c->radj16 && c->radj_owned) (void)hipFree(c->radj16);
+    if (c->runs) (void)hipFree(c->runs);
+    c->runs = nullptr;
+    c->runs_R = 0;
     if (c->adj16) (void)hipFree(c->adj16);
     if (c->deg32) (void)hipFree(c->deg32);
     if (c->ell16) (void)hipFree(c->ell16);
@@ -104,6 +107,38 @@ static void free_graph(sdnr_ctx *c)
 }
 
 static constexpr size_t kPad = SDNR_WAVE;
+
+// Sorted rows (stride-64 u16 rows padded with the sentinel V) as arithmetic
+// runs for dfs_runs.hip: greedy longest progression from each position,
+// strides <= 511, counts <= 64, a run word = start | stride << 16 | count <<
+// 25.  Returns the most runs a row needs; out gets R words per row.
+static int encode_runs(int32_t V, const std::vector<uint16_t> &rows, int R,
+                       std::vector<uint32_t> *out)
+{
+    int most = 0;
+    if (out) out->assign((((size_t)V + 1) * R + 3) & ~(size_t)3, 0u);
+    for (int32_t u = 0; u < V; ++u) {
+        const uint16_t *r = rows.data() + (size_t)u * SDNR_WAVE;
+        int n = 0;
+        while (n < SDNR_WAVE && r[n] != (uint16_t)V) ++n;
+        int nr = 0;
+        for (int i = 0; i < n;) {
+            int j = i, st = 0;
+            if (i + 1 < n && r[i + 1] - r[i] <= 511) {
+                st = r[i + 1] - r[i];
+                j = i + 1;
+                while (j + 1 < n && r[j + 1] - r[j] == st) ++j;
+            }
+            if (out && nr < R)
+                (*out)[(size_t)u * R + nr] = (uint32_t)r[i] | ((uint32_t)st << 16) |
+                                             ((uint32_t)(j - i + 1) << 25);
+            ++nr;
+            i = j + 1;
+        }
+        most = nr > most ? nr : most;
+    }
+    return most;
+}
 
 // device copy of `bytes` plus `pad` int32 entries of -1 behind them
 static int upload(int32_t **dst, const void *src, size_t bytes, size_t pad, hipStream_t s)
@@ -381,7 +416,7 @@ static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *
         const size_t rows = ((size_t)V + 1) * SDNR_WAVE;
         std::vector<uint16_t> a16(rows, (uint16_t)V), r16(rows, (uint16_t)V);
         std::vector<int32_t> indeg((size_t)V + 1, 0);
-        std::vector<uint32_t> d32((size_t)V + 1, 0u);
+        std::vector<uint32_t> d32(((size_t)V + 2) & ~(size_t)1, 0u);   // even: read in pairs
         for (int32_t u = 0; u < V; ++u) {
             const int32_t d = row_ptr[u + 1] - row_ptr[u];
             d32[(size_t)u] = (uint32_t)d;
@@ -419,6 +454,22 @@ static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *
                 if (he == hipSuccess)
                     he = hipMemcpyAsync(ctx->radj16, r16.data(), rows * 2, hipMemcpyHostToDevice,
                                         ctx->stream);
+            }
+        }
+        // the out-rows as arithmetic runs for the LDS-row DFS (dfs_runs.hip)
+        const char *rf = getenv("SDNROUTE_RUNS");                 // 0: off (A/B)
+        if (he == hipSuccess && maxin <= SDNR_WAVE && !(rf && !strcmp(rf, "0"))) {
+            const int m = encode_runs(V, a16, 0, nullptr);
+            const int R = m <= 2 ? 2 : (m <= 4 ? 4 : 0);
+            if (R) {
+                std::vector<uint32_t> w;
+                encode_runs(V, a16, R, &w);
+                he = hipMalloc(reinterpret_cast<void **>(&ctx->runs), w.size() * 4);
+                if (he == hipSuccess)
+                    he = hipMemcpyAsync(ctx->runs, w.data(), w.size() * 4, hipMemcpyHostToDevice,
+                                        ctx->stream);
+                if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
+                ctx->runs_R = R;
             }
         }
         if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);

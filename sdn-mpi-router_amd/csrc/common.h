@@ -59,6 +59,10 @@ struct sdnr_ctx {
     uint16_t *radj16 = nullptr;         // in-neighbour rows, same layout (== adj16 if symmetric)
     uint32_t *deg32 = nullptr;          // out-degrees of 0..V (sentinel V: 0)
     bool radj_owned = false;
+    // out-rows as arithmetic runs (dfs_runs.hip): (V+1) rows x runs_R words
+    // of start | stride << 16 | count << 25
+    uint32_t *runs = nullptr;
+    int32_t runs_R = 0;
 
     // grow-only device scratch / staging
     void *scratch = nullptr;
@@ -120,6 +124,11 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
                     int32_t *d_parent, int32_t *d_port, int32_t *d_hops,
                     uint32_t *d_tree,         // d_tree: packed layout instead of the three
                     bool slots = false);      // d_tree as parent | slot << 26
+// LDS-row DFS (dfs_runs.hip): usable when the run-encoded rows plus one
+// source's state fit a workgroup's LDS
+bool sdnr_dfs_runs_ok(const sdnr_ctx *ctx, bool hops);
+int sdnr_launch_dfs_runs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, int32_t *d_parent,
+                         int32_t *d_port, int32_t *d_hops, uint32_t *d_tree);
 int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
                          uint16_t *d_dist, int32_t *d_nh, int32_t *d_nh_port);
 int sdnr_launch_apsp(sdnr_ctx *ctx, uint16_t *d_dist);

@@ -1485,7 +1485,10 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
     constexpr int U = 4;                         // init / flush vertices per thread per step
     constexpr int S = NW - 1;                    // workers
     constexpr int RING = 512;                    // children in flight (u16)
-    constexpr int G = NW <= 4 ? 16 : 8;          // rows in flight per worker
+#ifndef SDNR_ASYNC_G
+#define SDNR_ASYNC_G 16
+#endif
+    constexpr int G = NW <= 4 ? SDNR_ASYNC_G : 8;   // rows in flight per worker
     constexpr unsigned kSpin = 1u << 22;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int VW = (V + 1 + 31) >> 5;
@@ -1747,7 +1750,8 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                 const int mine = lane < n ? (int)ring[(j + lane * S) & (RING - 1)] : V;
                 int r[G];
 #pragma unroll
-                for (int g = 0; g < G; ++g) r[g] = radj[(size_t)read_lane(mine, g) * 64 + lane];
+                for (int g = 0; g < G; ++g)
+                    r[g] = g < n ? (int)radj[(size_t)read_lane(mine, g) * 64 + lane] : V;
 #pragma unroll
                 for (int g = 0; g < G; ++g)
                     if (g < n && r[g] != V) atomicSub(&cnt[swz(r[g])], 1u);
@@ -2253,6 +2257,15 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
               ctx->port};
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
     const char *force = getenv("SDNROUTE_DFS_STRATEGY");
+    // rows in LDS as arithmetic runs (dfs_runs.hip), SDNROUTE_DFS_STRATEGY=
+    // runs: measured no faster than dfs_async_kernel, so
+    // opt-in
+    if (!(slots && packed) && sdnr_dfs_runs_ok(ctx, hops) && force && !strcmp(force, "runs")) {
+        int rc = sdnr_launch_dfs_runs(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree);
+        if (rc) return rc;
+        if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+        return SDNR_OK;
+    }
     const bool count_ok = ctx->adj16 != nullptr && ctx->radj16 != nullptr && V < 65535 &&
                           dfs_lds_bytes_count(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;
     const bool async_ok = count_ok && dfs_lds_bytes_async(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;

@@ -66,7 +66,7 @@ def _check_pairs(g, fabric, p, t, srcs):
         assert got == g.fdb(i), (g.name, i)
 
 
-@pytest.mark.parametrize("strategy", ["auto", "async", "count", "coop", "lds", "global",
+@pytest.mark.parametrize("strategy", ["auto", "runs", "async", "count", "coop", "lds", "global",
                                       "global-ring128", "global-nopack", "global-nosplit"])
 @pytest.mark.parametrize("ell", [True, False])
 @pytest.mark.parametrize("name", G.SMALL)
@@ -134,15 +134,86 @@ def test_dfs_slots_small(ctx, monkeypatch, name, strategy):
     np.testing.assert_array_equal(t, to)
 
 
-def test_dfs_packed_fullsize_k48(ctx):
+@pytest.mark.parametrize("strategy", ["runs", "async"])
+def test_dfs_packed_fullsize_k48(ctx, monkeypatch, strategy):
+    _strategy(monkeypatch, strategy)
     fabric = T.fat_tree(48)
     csr = fabric.csr()
     srcs = np.unique(fabric.host_table()[0]).astype(np.int32)
     ctx.upload(csr)
     tree = ctx.dfs_tables_packed(srcs)
-    assert ctx.last_kernel() == "dfs_async_kernel<4,packed>"
+    assert ctx.last_kernel() == ("dfs_runs_kernel<packed>" if strategy == "runs"
+                                 else "dfs_async_kernel<4,packed>")
     po, to, _ = O.dfs_tables(csr, srcs, with_hops=False, nthreads=NTHREADS)
     np.testing.assert_array_equal(tree, _pack(po, to))
+
+
+def _max_runs(csr):
+    """Most arithmetic runs a sorted row (out or in) needs -- the encoding of
+    capi.hip's encode_runs (strides <= 511)."""
+    def runs(row):
+        n, i, k = len(row), 0, 0
+        while i < n:
+            j = i
+            if i + 1 < n and row[i + 1] - row[i] <= 511:
+                st = row[i + 1] - row[i]
+                j = i + 1
+                while j + 1 < n and row[j + 1] - row[j] == st:
+                    j += 1
+            k += 1
+            i = j + 1
+        return k
+    V = csr.V
+    ins = [[] for _ in range(V)]
+    most = 0
+    for u in range(V):
+        row = [int(x) for x in csr.col[csr.row_ptr[u]:csr.row_ptr[u + 1]]]
+        most = max(most, runs(row))
+        for v in row:
+            ins[v].append(u)
+    return max([most] + [runs(r) for r in ins])
+
+
+# LDS-row kernel (dfs_runs.hip): every slot count / worker count / layout on
+# every small fabric whose rows encode in <= 4 runs
+@pytest.mark.parametrize("slots,workers", [(1, 1), (1, 3), (2, 2), (3, 3), (4, 3), (5, 2),
+                                           (8, 1)])
+@pytest.mark.parametrize("layout", ["int32", "hops", "packed"])
+@pytest.mark.parametrize("name", G.SMALL)
+def test_dfs_runs_small(ctx, monkeypatch, name, slots, workers, layout):
+    _strategy(monkeypatch, "runs")
+    monkeypatch.setenv("SDNROUTE_DFS_RUNS_SLOTS", str(slots))
+    monkeypatch.setenv("SDNROUTE_DFS_RUNS_S", str(workers))
+    csr = G.Golden(name).fabric().csr()
+    srcs = np.arange(csr.V, dtype=np.int32)
+    srcs = np.concatenate([srcs, srcs[::-1], srcs[:3]])      # more sources than slots
+    ctx.upload(csr)
+    po, to, ho = O.dfs_tables(csr, srcs, with_hops=True, nthreads=NTHREADS)
+    if layout == "packed":
+        got = ctx.dfs_tables_packed(srcs)
+        np.testing.assert_array_equal(got, _pack(po, to))
+    else:
+        p, t, h = ctx.dfs_tables(srcs, with_hops=layout == "hops")
+        np.testing.assert_array_equal(p, po)
+        np.testing.assert_array_equal(t, to)
+        if layout == "hops":
+            np.testing.assert_array_equal(h, ho)
+    if _max_runs(csr) <= 4:
+        assert ctx.last_kernel().startswith("dfs_runs_kernel"), ctx.last_kernel()
+
+
+@pytest.mark.parametrize("slots", [1, 5])
+@pytest.mark.parametrize("name", ["fat_tree_k48_sample", "dragonfly_a16_h8_p8_sample"])
+def test_dfs_runs_fullsize(ctx, monkeypatch, name, slots):
+    _strategy(monkeypatch, "runs")
+    monkeypatch.setenv("SDNROUTE_DFS_RUNS_SLOTS", str(slots))
+    g = G.Golden(name)
+    fabric = g.fabric()
+    csr = fabric.csr()
+    srcs = np.unique(fabric.host_table()[0]).astype(np.int32)
+    p, t = _check_dfs(ctx, csr, srcs)
+    assert ctx.last_kernel() == "dfs_runs_kernel<hops>"
+    _check_pairs(g, fabric, p, t, srcs)
 
 
 @pytest.mark.parametrize("waves", [2, 3, 4, 5, 6])
