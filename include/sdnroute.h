@@ -141,6 +141,18 @@ int sdnr_dfs_tables_packed(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc,
 int sdnr_dfs_tables_slots(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc,
                           uint32_t *tree, uint32_t flags);
 
+/* Pack n entries of int32 default-route tables (sdnr_dfs_tables' parent /
+ * port) into the 4-byte layouts above: layout SDNR_TREE_PORT16 = parent |
+ * port << 16 (sdnr_dfs_tables_packed), SDNR_TREE_SLOT = parent | slot << 26
+ * (sdnr_dfs_tables_slots; the slot is found in the uploaded CSR).  Device
+ * pointers only (flags must hold SDNR_DEVICE_PTRS); asynchronous on the
+ * context stream.  The route cache of the Python TopologyDB keeps its rows
+ * in these layouts (a third of the int32 tables' bytes). */
+#define SDNR_TREE_PORT16 1
+#define SDNR_TREE_SLOT   2
+int sdnr_tree_pack(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port,
+                   int64_t n, uint32_t *tree, int32_t layout, uint32_t flags);
+
 /* Shortest routes, find_route(src, dst, multiple=True) -> _find_routes_bfs
  * (topology_db.py:86-122, called from :168-180), as per-destination tables:
  * for every destination dst[i] and every vertex x

@@ -10,6 +10,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "common.h"
@@ -560,6 +562,31 @@ static int begin_call(sdnr_ctx *ctx, int32_t n, const void *ids, uint32_t flags,
 //    device's tables; the primary stream waits for every peer (join events).
 typedef int (*shard_launch_fn)(sdnr_ctx *c, const int32_t *ids, int32_t n, void *const out[3]);
 
+// Run `fn(k)` for shards 1..n-1 on host threads of their own and for shard 0
+// on the calling thread, then join: a shard launcher may block on the host
+// (the shortest-table level loops poll a host word per group of levels), so
+// the shards of a multi-device context must not wait for each other there.
+// The first failing shard's error (rc + its thread's message) is returned.
+extern "C++" template <typename Fn>
+static int on_shard_threads(int n, Fn fn)
+{
+    if (n == 1) return fn(0);
+    std::vector<int> rcs((size_t)n, SDNR_OK);
+    std::vector<std::string> msgs((size_t)n);
+    std::vector<std::thread> th;
+    for (int k = 1; k < n; ++k)
+        th.emplace_back([&, k] {
+            rcs[(size_t)k] = fn(k);
+            if (rcs[(size_t)k]) msgs[(size_t)k] = g_err;
+        });
+    rcs[0] = fn(0);
+    if (rcs[0]) msgs[0] = g_err;
+    for (auto &t : th) t.join();
+    for (int k = 0; k < n; ++k)
+        if (rcs[(size_t)k]) return sdnr_fail(rcs[(size_t)k], "%s", msgs[(size_t)k].c_str());
+    return SDNR_OK;
+}
+
 static int run_sharded(sdnr_ctx *ctx, const int32_t *ids, int32_t n, void *const out[3],
                        const size_t es[3], uint32_t flags, shard_launch_fn launch)
 {
@@ -575,16 +602,19 @@ static int run_sharded(sdnr_ctx *ctx, const int32_t *ids, int32_t n, void *const
         if (nctx == 1) return launch(ctx, ids, n, out);
         if (timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
         SDNR_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
-        for (int k = 1; k < nctx; ++k) {           // peers first: they run meanwhile
+        ctx->timed = false;                        // the span is timed around fork/join
+        rc = on_shard_threads(nctx, [&](int k) -> int {
             sdnr_ctx *c = sub(k);
             const int32_t lo = lo_of(k), cnt = hi_of(k) - lo;
-            if (cnt <= 0) continue;
             SDNR_HIP(hipSetDevice(c->device));
+            if (k == 0) return launch(ctx, ids, hi_of(0), out);
+            if (cnt <= 0) return SDNR_OK;
             SDNR_HIP(hipStreamWaitEvent(c->stream, ctx->ev_fork, 0));
             size_t need = 4 * (size_t)cnt + 256;
             for (int i = 0; i < 3; ++i)
                 if (out[i]) need += (size_t)cnt * V * es[i] + 256;
-            if ((rc = sdnr_reserve(&c->stage, &c->stage_bytes, need))) return rc;
+            int r;
+            if ((r = sdnr_reserve(&c->stage, &c->stage_bytes, need))) return r;
             Stage st{static_cast<char *>(c->stage)};
             int32_t *d_ids = static_cast<int32_t *>(st.take(4 * (size_t)cnt));
             void *d_out[3] = {nullptr, nullptr, nullptr};
@@ -593,56 +623,52 @@ static int run_sharded(sdnr_ctx *ctx, const int32_t *ids, int32_t n, void *const
             SDNR_HIP(hipMemcpyPeerAsync(d_ids, c->device, ids + lo, ctx->device, 4 * (size_t)cnt,
                                         c->stream));
             c->timed = false;
-            if ((rc = launch(c, d_ids, cnt, d_out))) return rc;
+            if ((r = launch(c, d_ids, cnt, d_out))) return r;
             for (int i = 0; i < 3; ++i)
                 if (out[i])
                     SDNR_HIP(hipMemcpyPeerAsync(static_cast<char *>(out[i]) + (size_t)lo * V * es[i],
                                                 ctx->device, d_out[i], c->device,
                                                 (size_t)cnt * V * es[i], c->stream));
             SDNR_HIP(hipEventRecord(c->ev_join, c->stream));
-        }
-        SDNR_HIP(hipSetDevice(ctx->device));
-        ctx->timed = false;                        // the span is timed around fork/join
-        rc = launch(ctx, ids, hi_of(0), out);
+            return SDNR_OK;
+        });
         ctx->timed = timed;
+        SDNR_HIP(hipSetDevice(ctx->device));
         if (rc) return rc;
         for (int k = 1; k < nctx; ++k)
             if (hi_of(k) > lo_of(k)) SDNR_HIP(hipStreamWaitEvent(ctx->stream, sub(k)->ev_join, 0));
         if (timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
         return SDNR_OK;
     }
-    // host buffers: stage + launch everywhere, then copy out, then wait
+    // host buffers: stage + launch everywhere (one host thread per shard),
+    // copy out, then wait
     void *d_outs[64][3] = {};
     if (nctx > 64) return sdnr_fail(SDNR_ERR_INVAL, "more than 64 devices");
-    for (int k = 0; k < nctx; ++k) {
+    rc = on_shard_threads(nctx, [&](int k) -> int {
         sdnr_ctx *c = sub(k);
         const int32_t lo = lo_of(k), cnt = hi_of(k) - lo;
-        if (cnt <= 0) continue;
+        if (cnt <= 0) return SDNR_OK;
         SDNR_HIP(hipSetDevice(c->device));
         size_t need = 4 * (size_t)cnt + 256;
         for (int i = 0; i < 3; ++i)
             if (out[i]) need += (size_t)cnt * V * es[i] + 256;
-        if ((rc = sdnr_reserve(&c->stage, &c->stage_bytes, need))) return rc;
+        int r;
+        if ((r = sdnr_reserve(&c->stage, &c->stage_bytes, need))) return r;
         Stage st{static_cast<char *>(c->stage)};
         int32_t *d_ids = static_cast<int32_t *>(st.take(4 * (size_t)cnt));
         for (int i = 0; i < 3; ++i)
             if (out[i]) d_outs[k][i] = st.take((size_t)cnt * V * es[i]);
         SDNR_HIP(hipMemcpyAsync(d_ids, ids + lo, 4 * (size_t)cnt, hipMemcpyHostToDevice, c->stream));
         c->timed = k == 0 && nctx == 1 && timed;  // multi: shard 0 alone is not the span
-        if ((rc = launch(c, d_ids, cnt, d_outs[k]))) return rc;
-    }
-    for (int k = 0; k < nctx; ++k) {
-        sdnr_ctx *c = sub(k);
-        const int32_t lo = lo_of(k), cnt = hi_of(k) - lo;
-        if (cnt <= 0) continue;
-        SDNR_HIP(hipSetDevice(c->device));
+        if ((r = launch(c, d_ids, cnt, d_outs[k]))) return r;
         for (int i = 0; i < 3; ++i)
             if (out[i])
                 SDNR_HIP(hipMemcpyAsync(static_cast<char *>(out[i]) + (size_t)lo * V * es[i],
                                         d_outs[k][i], (size_t)cnt * V * es[i],
                                         hipMemcpyDeviceToHost, c->stream));
-    }
-    int first = SDNR_OK;
+        return SDNR_OK;
+    });
+    int first = rc;
     for (int k = 0; k < nctx; ++k) {
         sdnr_ctx *c = sub(k);
         SDNR_HIP(hipSetDevice(c->device));
@@ -718,6 +744,28 @@ int sdnr_dfs_tables_slots(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc, uint3
     void *const out[3] = {tree, nullptr, nullptr};
     const size_t es[3] = {4, 0, 0};
     return run_sharded(ctx, src, nsrc, out, es, flags, shard_dfs_slots);
+}
+
+int sdnr_tree_pack(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port, int64_t n,
+                   uint32_t *tree, int32_t layout, uint32_t flags)
+{
+    CHECK_CTX(ctx);
+    if (ctx->V < 0) return sdnr_fail(SDNR_ERR_STATE, "sdnr_tree_pack: no graph uploaded");
+    if (!(flags & SDNR_DEVICE_PTRS))
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_tree_pack: device pointers only");
+    if (n < 0 || (n > 0 && (!parent || !tree || (layout == SDNR_TREE_PORT16 && !port))))
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_tree_pack: null table");
+    if (layout == SDNR_TREE_PORT16 && (ctx->V > 0xFFFF || !ctx->port16))
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_tree_pack: port16 needs V <= 65535 and ports "
+                         "< 0xFFFF (V=%d)", ctx->V);
+    if (layout == SDNR_TREE_SLOT && (ctx->V > (1 << 26) - 1 || ctx->max_deg > 63))
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_tree_pack: slots need V < 2^26 and rows of "
+                         "<= 63 links (V=%d)", ctx->V);
+    if (layout != SDNR_TREE_PORT16 && layout != SDNR_TREE_SLOT)
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_tree_pack: layout %d", layout);
+    if (n == 0 || ctx->V == 0) return SDNR_OK;
+    SDNR_HIP(hipSetDevice(ctx->device));
+    return sdnr_launch_tree_pack(ctx, parent, port, (size_t)n, tree, layout == SDNR_TREE_SLOT);
 }
 
 int sdnr_shortest_tables(sdnr_ctx *ctx, const int32_t *dst, int32_t ndst, uint16_t *dist,

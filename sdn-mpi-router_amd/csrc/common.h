@@ -124,6 +124,9 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
                     int32_t *d_parent, int32_t *d_port, int32_t *d_hops,
                     uint32_t *d_tree,         // d_tree: packed layout instead of the three
                     bool slots = false);      // d_tree as parent | slot << 26
+// int32 trees -> parent | port << 16 or parent | slot << 26 (dfs.hip)
+int sdnr_launch_tree_pack(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port, size_t n,
+                          uint32_t *tree, bool slots);
 // LDS-row DFS (dfs_runs.hip): usable when the run-encoded rows plus one
 // source's state fit a workgroup's LDS
 bool sdnr_dfs_runs_ok(const sdnr_ctx *ctx, bool hops);

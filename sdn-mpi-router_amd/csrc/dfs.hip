@@ -2214,6 +2214,20 @@ static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, in
     return SDNR_OK;
 }
 
+int sdnr_launch_tree_pack(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port, size_t n,
+                          uint32_t *tree, bool slots)
+{
+    const int V = ctx->V;
+    if (slots)
+        hipLaunchKernelGGL(dfs_slot_pack_kernel, dim3(ctx->num_cus * 8), dim3(256), 0,
+                           ctx->stream, n, V, parent, ctx->row_ptr, ctx->col, tree);
+    else
+        hipLaunchKernelGGL(dfs_pack_kernel, dim3(ctx->num_cus * 8), dim3(256), 0, ctx->stream,
+                           n, parent, port, tree);
+    SDNR_HIP(hipGetLastError());
+    return SDNR_OK;
+}
+
 int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
                     int32_t *d_parent, int32_t *d_port, int32_t *d_hops, uint32_t *d_tree,
                     bool slots)

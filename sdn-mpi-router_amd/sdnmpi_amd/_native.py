@@ -27,6 +27,8 @@ TIMING = 0x2
 UNREACHED = -1
 DIST_INF = 0xFFFF
 TREE_NONE = 0xFFFFFFFF
+TREE_PORT16 = 1          # parent | port << 16 (sdnr_dfs_tables_packed)
+TREE_SLOT = 2            # parent | slot << 26 (sdnr_dfs_tables_slots)
 ABI_VERSION = 1
 
 # every entry point declared in include/sdnroute.h
@@ -34,7 +36,7 @@ EXPORTED_SYMBOLS = (
     "sdnr_abi_version", "sdnr_last_error", "sdnr_device_count", "sdnr_create",
     "sdnr_create_multi", "sdnr_device_list", "sdnr_destroy", "sdnr_set_stream", "sdnr_synchronize", "sdnr_graph_upload",
     "sdnr_graph_info", "sdnr_dfs_tables", "sdnr_dfs_tables_packed", "sdnr_dfs_tables_slots",
-    "sdnr_shortest_tables",
+    "sdnr_tree_pack", "sdnr_shortest_tables",
     "sdnr_apsp", "sdnr_route_offsets", "sdnr_route_expand", "sdnr_ecmp_counts",
     "sdnr_ecmp_routes",
     "sdnr_last_kernel_ms", "sdnr_last_kernel", "sdnr_last_launches", "sdnr_edge_ports",
@@ -77,6 +79,7 @@ def _bind(L):
         "sdnr_dfs_tables": ([vp, vp, i32, vp, vp, vp, u32], c_int),
         "sdnr_dfs_tables_packed": ([vp, vp, i32, vp, u32], c_int),
         "sdnr_dfs_tables_slots": ([vp, vp, i32, vp, u32], c_int),
+        "sdnr_tree_pack": ([vp, vp, vp, ctypes.c_int64, vp, i32, u32], c_int),
         "sdnr_shortest_tables": ([vp, vp, i32, vp, vp, vp, u32], c_int),
         "sdnr_apsp": ([vp, vp, u32], c_int),
         "sdnr_route_offsets": ([vp, vp, i32, vp, vp, i32, vp, u32], c_int),
@@ -378,6 +381,13 @@ class Context(object):
         flags = DEVICE_PTRS | (TIMING if timing else 0)
         _check(self._lib.sdnr_dfs_tables_slots(self._h, ctypes.c_void_p(src_ptr), int(nsrc),
                                                ctypes.c_void_p(tree_ptr), flags))
+
+    def tree_pack_device(self, parent_ptr, port_ptr, n, tree_ptr, layout):
+        """int32 parent/port tables (device) -> 4-byte trees (sdnr_tree_pack)."""
+        _check(self._lib.sdnr_tree_pack(self._h, ctypes.c_void_p(parent_ptr),
+                                        ctypes.c_void_p(port_ptr) if port_ptr else None,
+                                        int(n), ctypes.c_void_p(tree_ptr), int(layout),
+                                        DEVICE_PTRS))
 
     def shortest_tables_device(self, dst_ptr, ndst, dist_ptr, nh_ptr=0, nh_port_ptr=0,
                                timing=False):

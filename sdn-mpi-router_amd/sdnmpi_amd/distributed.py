@@ -107,16 +107,22 @@ def sharded_route_tables(db, mode="dfs", group=None):
     t = db.route_tables(mode, vertices=hv[lo:hi])
     names = ("parent", "port", "hops") if mode == "dfs" else ("dist", "nh", "nh_port")
     out = dict(t)
+    # RCCL moves device tensors only: the rank's shard goes to its GPU (one
+    # process per GPU, torch's current device) and the gathered table back
+    nccl = dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", torch.cuda.current_device()) if nccl else None
     for name in names:
         a = t[name]
         pad = np.full((per, a.shape[1]), 0xFFFF if a.dtype == np.uint16 else -1, a.dtype)
         pad[: a.shape[0]] = a
         loc = torch.from_numpy(pad.view(np.int16) if a.dtype == np.uint16 else pad)
-        if loc.dtype == torch.int16:                        # gloo: move the bytes
-            g = all_gather_rows(loc.view(torch.uint8)).view(torch.int16)
+        if dev is not None:
+            loc = loc.to(dev)
+        if loc.dtype == torch.int16:                        # no 16-bit integers: move bytes
+            g = all_gather_rows(loc.view(torch.uint8), group=group).view(torch.int16)
         else:
-            g = all_gather_rows(loc)
-        g = unpad(g, len(hv)).numpy()
+            g = all_gather_rows(loc, group=group)
+        g = unpad(g, len(hv)).cpu().numpy()
         out[name] = g.view(np.uint16) if a.dtype == np.uint16 else g
     out["sources" if mode == "dfs" else "destinations"] = np.asarray(hv, np.int32)
     return out

@@ -7,11 +7,24 @@ device (torch is only the device-memory plumbing here) and ``TableCache``
 keeps, per uploaded graph, the per-source DFS tables (default route,
 reference ``_find_route_dfs``, ``sdnmpi/util/topology_db.py:59-84``) and the
 per-destination shortest tables (``_find_routes_bfs``, :86-122) computed so
-far, within a byte budget.  A single ``find_route`` copies back one table row
-(V entries, kept in a small host cache), a batch is expanded on the device.
-Expansion follows the reference's ``_route_to_fdb`` (:127-138): one
-``(dpid, out_port)`` per switch on the path, the last one being the
-destination switch's host port or ``OFPP_LOCAL``.
+far, within a byte budget, in a fixed-capacity pool of compact rows:
+
+* default route: one 4-byte tree word per vertex -- ``parent | port << 16``
+  (V <= 65535, 16-bit ports: sdnr_dfs_tables_packed's layout) or ``parent |
+  slot << 26`` (sdnr_dfs_tables_slots') -- plus the tree depth (u16 for
+  V <= 65535, else int32): 6 bytes per entry where the int32 parent / port /
+  hops tables take 12 (8 on fabrics above 65,535 switches);
+* shortest route: u16 distance plus the next hop (u16 for V <= 65535): 4
+  bytes per entry; the next hop's port is looked up in the CSR on demand.
+
+Slots are taken from a free list and given back on eviction or when a graph
+change invalidates the row; no operation copies the pool (it grows by
+doubling up to the budget), free slots hold all-unreached rows.  A single
+``find_route`` copies back one table row (V entries, kept in a small host
+cache), a batch is expanded on the device.  Expansion follows the
+reference's ``_route_to_fdb`` (:127-138): one ``(dpid, out_port)`` per switch
+on the path, the last one being the destination switch's host port or
+``OFPP_LOCAL``.
 
 The cache is storage-agnostic: an engine may hand back numpy arrays instead
 (the CPU tests' oracle-backed double), and every array operation below
@@ -27,13 +40,17 @@ from . import _native
 from .graph import empty_csr
 
 __all__ = ["RouteEngine", "TableCache", "tree_path", "expand_tree_paths",
-           "shortest_paths_lex", "DEFAULT_TABLE_BUDGET"]
+           "shortest_paths_lex", "DEFAULT_TABLE_BUDGET", "tree_layout", "dfs_row_bytes",
+           "sp_row_bytes"]
 
 # bytes of device tables one TableCache keeps per route mode before it
 # evicts rows (SDNROUTE_TABLE_BUDGET overrides); the torus 32^3 default-route
-# tables of every source are 12.9 GB, Jellyfish 100k's would be 120 GB
+# tables of every source take 6.4 GB in the pool, Jellyfish 100k's 80 GB
 DEFAULT_TABLE_BUDGET = int(os.environ.get("SDNROUTE_TABLE_BUDGET", str(24 << 30)))
 HOST_ROW_CACHE = 256            # table rows kept on the host for find_route
+COMPUTE_ROWS = 4096             # rows per engine call when filling the pool
+
+PORT16, SLOT, INT32 = "port16", "slot", "int32"
 
 
 # ------------------------------------------------------- array dispatch --
@@ -52,15 +69,6 @@ def _take(a, idx):
     return a.index_select(0, torch.as_tensor(idx, dtype=torch.int64, device=a.device))
 
 
-def _cat(blocks):
-    if blocks[0] is None:
-        return None
-    if _is_np(blocks[0]):
-        return np.concatenate(blocks)
-    import torch
-    return torch.cat(blocks)
-
-
 def _host(a):
     if a is None or _is_np(a):
         return a
@@ -71,6 +79,133 @@ def _nbytes(a):
     if a is None:
         return 0
     return a.nbytes if _is_np(a) else a.element_size() * a.numel()
+
+
+def _i64(a):
+    return a.astype(np.int64) if _is_np(a) else a.to(dtype=_torch().int64)
+
+
+def _torch():
+    import torch
+    return torch
+
+
+# ------------------------------------------------------- compact layouts --
+
+def tree_layout(csr):
+    """4-byte tree layout the cache keeps default-route rows in."""
+    V = csr.V
+    port = np.asarray(csr.port)
+    if V <= 0xFFFF and (port.size == 0 or (port.min() >= 0 and port.max() < 0xFFFF)):
+        return PORT16
+    if V < (1 << 26) and csr.max_degree() <= 63:
+        return SLOT
+    return INT32
+
+
+def _hops_dtype(V):
+    return "int16" if V <= 0xFFFF else "int32"
+
+
+def _nh_dtype(V):
+    return "int16" if V <= 0xFFFF else "int32"
+
+
+def dfs_row_bytes(csr):
+    """Bytes of one default-route row in the cache."""
+    lay = tree_layout(csr)
+    hb = 2 if csr.V <= 0xFFFF else 4
+    return (4 + hb if lay != INT32 else 12) * csr.V
+
+
+def sp_row_bytes(csr):
+    return (2 + (2 if csr.V <= 0xFFFF else 4)) * csr.V
+
+
+def _u16(a):
+    """u16 values stored in int16 (0xFFFF: -1) as int64."""
+    x = _i64(a) & 0xFFFF
+    return (x - ((x == 0xFFFF) * 0x10000)) if _is_np(x) else x.masked_fill(x == 0xFFFF, -1)
+
+
+class Wide(object):
+    """Read view of a compact table: indexing returns int64 values (u16
+    planes widened, 0xFFFF -> -1; tree words decoded to parents)."""
+
+    def __init__(self, arr, kind):
+        self.arr = arr
+        self.kind = kind               # "u16" | "u16raw" | "int" | PORT16 | SLOT
+        self.shape = arr.shape
+
+    def __getitem__(self, idx):
+        w = self.arr[idx]
+        if self.kind == "u16":
+            return _u16(w)
+        if self.kind == "u16raw":                  # distances: 0xFFFF stays INF
+            return _i64(w) & 0xFFFF
+        if self.kind == "int":
+            return _i64(w)
+        return tree_parent(w, self.kind)
+
+
+def tree_parent(w, layout):
+    """Parents (int64, -1 unreached) of tree words (int32 storage)."""
+    x = _i64(w) & 0xFFFFFFFF
+    if layout == PORT16:
+        p = x & 0xFFFF
+        bad = p == 0xFFFF
+    else:
+        p = x & 0x3FFFFFF
+        bad = x == 0xFFFFFFFF
+    if _is_np(p):
+        p[bad] = -1
+        return p
+    return p.masked_fill(bad, -1)
+
+
+def tree_port(w, layout, row_ptr, port, parent=None):
+    """Ports (int64, -1 for the root / unreached) of tree words.  Slot trees
+    look the port up in the CSR (row_ptr / port arrays of the tree's type)."""
+    x = _i64(w) & 0xFFFFFFFF
+    if layout == PORT16:
+        t = x >> 16
+        return _where(t == 0xFFFF, -1, t)
+    slot = x >> 26
+    par = tree_parent(w, layout) if parent is None else parent
+    none = (par < 0) | (slot == 63)
+    if _is_np(x):
+        pz = np.where(none, 0, par)
+        idx = np.where(none, 0, row_ptr[pz] + slot)
+        return np.where(none, -1, np.asarray(port, np.int64)[idx])
+    pz = par.masked_fill(none, 0)
+    idx = (row_ptr[pz] + slot).masked_fill(none, 0)
+    return port[idx].to(x.dtype).masked_fill(none, -1)
+
+
+def _where(c, a, b):
+    if _is_np(b):
+        return np.where(c, a, b)
+    return b.masked_fill(c, a)
+
+
+def pack_host_tree(parent, port, csr, layout):
+    """Host (numpy) tables -> tree words (int32 storage): the test double's
+    counterpart of sdnr_tree_pack."""
+    p = np.asarray(parent, np.int64)
+    if layout == PORT16:
+        t = (p & 0xFFFF) | ((np.asarray(port, np.int64) & 0xFFFF) << 16)
+    else:
+        V = csr.V
+        rp = np.asarray(csr.row_ptr, np.int64)
+        src = np.repeat(np.arange(V, dtype=np.int64), np.diff(rp))
+        keys = src * V + np.asarray(csr.col, np.int64)
+        v = np.broadcast_to(np.arange(V, dtype=np.int64), p.shape)
+        ok = p >= 0
+        e = np.searchsorted(keys, np.where(ok, p, 0) * V + v)
+        slot = np.where(ok, e - rp[np.where(ok, p, 0)], 0)
+        slot = np.where(p == v, 63, slot)
+        t = np.where(ok, p | (slot << 26), 0xFFFFFFFF)
+    return (t & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
 
 
 class RouteEngine(object):
@@ -85,6 +220,7 @@ class RouteEngine(object):
         self.devices = self.ctx.devices
         self.dev = torch.device("cuda", self.devices[0])
         self._loaded = None
+        self._csr_dev = None        # (export, row_ptr int64, port int32) on the device
 
     # -- plumbing -------------------------------------------------------
     def _ready(self):
@@ -103,6 +239,16 @@ class RouteEngine(object):
             self.ctx.upload(export.csr if export.csr.V else empty_csr())
             self._loaded = export
 
+    def csr_device(self, export):
+        """(row_ptr int64, port int32) of the export on the device (slot trees
+        look their ports up here)."""
+        if self._csr_dev is None or self._csr_dev[0] is not export:
+            t = self._torch
+            c = export.csr
+            self._csr_dev = (export, t.from_numpy(np.asarray(c.row_ptr, np.int64)).to(self.dev),
+                             t.from_numpy(np.asarray(c.port, np.int32)).to(self.dev))
+        return self._csr_dev[1], self._csr_dev[2]
+
     # -- tables (device-resident) ---------------------------------------
     def dfs_tables(self, export, srcs, with_hops=True):
         """(parent, port, hops) int32 [S, V] tensors on the primary device."""
@@ -119,6 +265,19 @@ class RouteEngine(object):
                                        hop.data_ptr() if hop is not None else 0)
             self.ctx.synchronize()          # also raises on a tripped kernel watchdog
         return par, prt, hop
+
+    def pack_trees(self, export, parent, port, layout):
+        """int32 tables -> tree words (int32 tensor), sdnr_tree_pack."""
+        self.load(export)
+        tree = self._torch.empty_like(parent)
+        n = parent.numel()
+        if n:
+            self._ready()
+            self.ctx.tree_pack_device(parent.data_ptr(), port.data_ptr(), n, tree.data_ptr(),
+                                      _native.TREE_PORT16 if layout == PORT16
+                                      else _native.TREE_SLOT)
+            self.ctx.synchronize()
+        return tree
 
     def shortest_tables(self, export, dsts):
         """(dist int16 [D, V] holding u16, nh, nh_port int32) on the device."""
@@ -186,33 +345,30 @@ class RouteEngine(object):
     def expand(self, export, tables, rows, dsts, last_port):
         """Flow entries of many pairs (routes.hip) from device tables:
         (offsets int64 [n+1], switch ids int32, ports int32) on the host.
-        Only the table rows the pairs use go through the expansion."""
+        ``tables`` = (parent, port, hops) [k, V] of the rows the pairs use
+        (int32, or any integer view the cache decodes to)."""
         self.load(export)
         t = self._torch
-        parent, port, hops = tables
+        par, prt, hop = (a.to(t.int32).contiguous() for a in tables)
         rows = np.asarray(rows, np.int64)
         n = rows.shape[0]
         off = np.zeros(n + 1, np.int64)
         if n == 0:
             return off, np.zeros(0, np.int32), np.zeros(0, np.int32)
-        urows, inv = np.unique(rows, return_inverse=True)
-        sel = t.as_tensor(urows, dtype=t.int64, device=self.dev)
-        par = parent.index_select(0, sel)
-        prt = port.index_select(0, sel)
-        hop = hops.index_select(0, sel)
-        d_rows = self._ids(inv)
+        nrows = int(par.shape[0])
+        d_rows = self._ids(rows)
         d_dsts = self._ids(dsts)
         d_last = self._ids(last_port)
         d_off = t.empty(n + 1, dtype=t.int64, device=self.dev)
         self._ready()
         self.ctx.route_offsets_device(hop.data_ptr(), d_rows.data_ptr(), d_dsts.data_ptr(), n,
-                                      d_off.data_ptr(), nrows=len(urows))
+                                      d_off.data_ptr(), nrows=nrows)
         self.ctx.synchronize()
         off = d_off.cpu().numpy()
         total = int(off[-1])
         sw = t.empty(max(total, 1), dtype=t.int32, device=self.dev)
         hp = t.empty(max(total, 1), dtype=t.int32, device=self.dev)
-        self.ctx.expand_routes_device(par.data_ptr(), prt.data_ptr(), len(urows),
+        self.ctx.expand_routes_device(par.data_ptr(), prt.data_ptr(), nrows,
                                       d_rows.data_ptr(), d_dsts.data_ptr(), d_last.data_ptr(), n,
                                       d_off.data_ptr(), sw.data_ptr(), hp.data_ptr())
         self.ctx.synchronize()
@@ -227,70 +383,118 @@ class RouteEngine(object):
         self.ctx.close()
 
 
-class _Rows(object):
-    """Table rows of one route mode (tuple of [n, V] arrays, one row per
-    vertex), appended in blocks, merged on use, bounded by a byte budget with
-    oldest-first eviction."""
+class _Pool(object):
+    """Table rows of one route mode in a fixed-capacity store.
 
-    def __init__(self, budget):
+    ``arrays`` is a tuple of [capacity, V] tables (device tensors or numpy);
+    a row lives in a slot, ``row`` maps vertex -> slot, ``lru`` orders the
+    vertices oldest first.  Adding takes slots from the free list (evicting
+    the oldest unprotected rows when the budget is full), dropping gives
+    them back and refills them with the ``blank`` row (all unreached), so a
+    test over the whole store never sees garbage.  The store grows by
+    doubling up to ``cap`` rows; it is never concatenated, re-indexed or
+    copied otherwise."""
+
+    def __init__(self, budget, row_bytes, blanks):
         self.budget = budget
-        self.blocks = []           # list of tuples, merged lazily
-        self.order = []            # vertex of every row, row order
-        self.row = {}              # vertex -> row
-        self.row_bytes = 0
-        self.host = collections.OrderedDict()   # vertex -> host row tuple (LRU)
+        self.row_bytes = row_bytes
+        self.blanks = blanks                   # fill value per table
+        self.arrays = None
+        self.size = 0                          # allocated slots
+        self.row = {}
+        self.lru = collections.OrderedDict()
+        self.free = []
+        self.host = collections.OrderedDict()  # vertex -> host row tuple (LRU)
 
     def __contains__(self, v):
         return v in self.row
 
     def __len__(self):
-        return len(self.order)
+        return len(self.row)
 
     def cap(self):
         """Rows the budget holds (at least one)."""
         return max(1, self.budget // self.row_bytes) if self.row_bytes else 1 << 62
 
     def tables(self):
-        if len(self.blocks) > 1:
-            self.blocks = [tuple(_cat([b[i] for b in self.blocks])
-                                 for i in range(len(self.blocks[0])))]
-        return self.blocks[0] if self.blocks else None
+        return self.arrays
 
-    def add(self, verts, tabs):
-        if not verts:
-            return
-        if not self.row_bytes:
-            self.row_bytes = sum(_nbytes(a) for a in tabs) // len(verts)
-        base = len(self.order)
-        self.blocks.append(tabs)
-        for i, v in enumerate(verts):
-            self.row[v] = base + i
-        self.order.extend(verts)
+    def slot_vertices(self):
+        """int64 numpy [size]: vertex of every slot, -1 for free ones."""
+        s = np.full(self.size, -1, np.int64)
+        if self.row:
+            s[np.fromiter(self.row.values(), np.int64, len(self.row))] = \
+                np.fromiter(self.row.keys(), np.int64, len(self.row))
+        return s
 
-    def keep(self, mask):
-        """Keep the rows where ``mask`` (bool numpy [n]) is set."""
-        idx = np.nonzero(np.asarray(mask, bool))[0]
-        if idx.size == len(self.order):
+    def _grow(self, need, like):
+        """Make at least ``need`` slots exist (doubling, at most cap)."""
+        if need <= self.size:
             return
-        tabs = self.tables()
-        self.blocks = [tuple(_take(a, idx) for a in tabs)] if idx.size else []
-        self.order = [self.order[i] for i in idx.tolist()]
-        self.row = {v: i for i, v in enumerate(self.order)}
-        self.host.clear()
+        new = min(self.cap(), max(need, 2 * self.size, 16))
+        fresh = []
+        for a, b in zip(like, self.blanks):
+            shape = (new,) + tuple(a.shape[1:])
+            if _is_np(a):
+                z = np.full(shape, b, a.dtype)
+            else:
+                z = _torch().full(shape, b, dtype=a.dtype, device=a.device)
+            fresh.append(z)
+        if self.arrays is not None:
+            for z, a in zip(fresh, self.arrays):
+                z[:self.size] = a
+        self.free.extend(range(new - 1, self.size - 1, -1))   # lowest slot popped first
+        self.arrays = tuple(fresh)
+        self.size = new
 
     def make_room(self, n, protect):
         """Evict the oldest rows not in ``protect`` until n more fit."""
-        over = len(self.order) + n - self.cap()
+        over = len(self.row) + n - self.cap()
         if over <= 0:
             return
-        mask = np.ones(len(self.order), bool)
-        for i, v in enumerate(self.order):
+        out = []
+        for v in self.lru:
             if over <= 0:
                 break
             if v not in protect:
-                mask[i] = False
+                out.append(v)
                 over -= 1
-        self.keep(mask)
+        self.drop(out)
+
+    def drop(self, verts):
+        """Give the slots of ``verts`` back (blank rows)."""
+        slots = [self.row.pop(v) for v in verts if v in self.row]
+        for v in verts:
+            self.lru.pop(v, None)
+            self.host.pop(v, None)
+        if not slots:
+            return
+        idx = np.asarray(slots, np.int64)
+        for a, b in zip(self.arrays, self.blanks):
+            if _is_np(a):
+                a[idx] = b
+            else:
+                a[_torch().as_tensor(idx, device=a.device)] = b
+        self.free.extend(slots)
+
+    def add(self, verts, tabs):
+        """Store rows ``tabs`` ([n, V] each) for ``verts`` (room was made)."""
+        if not verts:
+            return
+        self._grow(len(self.row) + len(verts), tabs)
+        slots = [self.free.pop() for _ in verts]
+        idx = np.asarray(slots, np.int64)
+        contiguous = bool(np.all(np.diff(idx) == 1))
+        for a, t in zip(self.arrays, tabs):
+            if contiguous:
+                a[slots[0]:slots[0] + len(slots)] = t
+            elif _is_np(a):
+                a[idx] = t
+            else:
+                a.index_copy_(0, _torch().as_tensor(idx, device=a.device), t)
+        for v, s in zip(verts, slots):
+            self.row[v] = s
+            self.lru[v] = None
 
     def host_row(self, v):
         """One row of every table, on the host (small LRU)."""
@@ -299,8 +503,7 @@ class _Rows(object):
             self.host.move_to_end(v)
             return hit
         r = self.row[v]
-        tabs = self.tables()
-        rows = tuple(_host(a[r:r + 1])[0] if a is not None else None for a in tabs)
+        rows = tuple(_host(a[r:r + 1])[0] for a in self.arrays)
         self.host[v] = rows
         if len(self.host) > HOST_ROW_CACHE:
             self.host.popitem(last=False)
@@ -308,20 +511,24 @@ class _Rows(object):
 
 
 class TableCache(object):
-    """Per-graph cache of computed table rows, keyed by dense vertex id."""
+    """Per-graph cache of computed table rows, keyed by dense vertex id, in
+    compact pools (module docstring).  ``retarget`` follows a graph change
+    over the same vertex set in place: the rows the change can alter are
+    dropped (:mod:`sdnmpi_amd.incremental`), the rest stay in their slots."""
 
     def __init__(self, export, budget=None):
         self.export = export
         b = DEFAULT_TABLE_BUDGET if budget is None else int(budget)
-        V = export.csr.V
-        self.dfs = _Rows(b)        # (parent, port, hops) per source
-        self.sp = _Rows(b)         # (dist, nh, nh_port) per destination
-        self.dfs.row_bytes = 12 * V    # int32 parent + port + hops
-        self.sp.row_bytes = 10 * V     # u16 dist + int32 nh + nh_port
+        csr = export.csr
+        self.layout = tree_layout(csr)
+        self.V = csr.V
+        dfs_blank = (-1, -1, -1) if self.layout == INT32 else (-1, -1)
+        self.dfs = _Pool(b, dfs_row_bytes(csr), dfs_blank)
+        self.sp = _Pool(b, sp_row_bytes(csr), (-1, -1))
         self.rows_computed = 0     # rows sent to the GPU (both modes)
         self.rows_inherited = 0    # rows kept across a graph change
 
-    # back-compat views used by callers/tests
+    # vertex -> row (slot) maps
     @property
     def dfs_row(self):
         return self.dfs.row
@@ -330,54 +537,133 @@ class TableCache(object):
     def sp_row(self):
         return self.sp.row
 
-    def inherit(self, old, diff):
-        """Keep the rows of ``old`` (a cache of the previous graph over the
-        same vertex set) that the link changes in ``diff`` cannot alter
-        (:mod:`sdnmpi_amd.incremental`); the rest are recomputed on demand.
-        The tests run where the tables live (device tensors stay on the
-        device)."""
-        from .incremental import dfs_rows_affected, sp_rows_affected
-        self.dfs.budget, self.sp.budget = old.dfs.budget, old.sp.budget
-        for mine, theirs, test in (
-                (self.dfs, old.dfs, lambda t, vs: dfs_rows_affected(t[0], t[2], vs, diff)),
-                (self.sp, old.sp, lambda t, vs: sp_rows_affected(t[0], t[1], diff))):
-            tabs = theirs.tables()
-            if tabs is None or tabs[1] is None or (mine is self.dfs and tabs[2] is None):
-                continue
-            verts = np.asarray(theirs.order, np.int64)
-            keep = ~np.asarray(test(tabs, verts), bool)
-            if keep.any():
-                idx = np.nonzero(keep)[0]
-                mine.add(verts[idx].tolist(), tuple(_take(a, idx) for a in tabs))
-                mine.row_bytes = theirs.row_bytes
-                self.rows_inherited += int(idx.size)
+    # -- decoded views ---------------------------------------------------
+    def dfs_parent_hops(self):
+        """(parent, hops) read views over the whole DFS pool (Wide)."""
+        a = self.dfs.tables()
+        if a is None:
+            return None, None
+        if self.layout == INT32:
+            return Wide(a[0], "int"), Wide(a[2], "int")
+        return Wide(a[0], self.layout), Wide(a[1], "u16" if self.V <= 0xFFFF else "int")
 
+    def dfs_int32(self, slots, engine=None):
+        """(parent, port, hops) int32-valued int64 tables of pool slots
+        ``slots`` (array type of the pool)."""
+        a = self.dfs.tables()
+        sel = [_take(x, slots) for x in a]
+        if self.layout == INT32:
+            return tuple(_i64(x) for x in sel)
+        par = tree_parent(sel[0], self.layout)
+        if self.layout == PORT16:
+            prt = tree_port(sel[0], PORT16, None, None)
+        elif _is_np(sel[0]):
+            c = self.export.csr
+            prt = tree_port(sel[0], SLOT, np.asarray(c.row_ptr, np.int64), c.port, par)
+        else:
+            rp, pt = engine.csr_device(self.export)
+            prt = tree_port(sel[0], SLOT, rp, pt, par)
+        hop = _u16(sel[1]) if self.V <= 0xFFFF else _i64(sel[1])
+        return par, prt, hop
+
+    def dfs_host_row(self, v):
+        """(parent, port) int64 numpy rows of source v (host LRU)."""
+        row = self.dfs.host_row(v)
+        if self.layout == INT32:
+            return row[0], row[1]
+        c = self.export.csr
+        par = tree_parent(row[0], self.layout)
+        return par, tree_port(row[0], self.layout, np.asarray(c.row_ptr, np.int64), c.port, par)
+
+    def sp_dist_host_row(self, d):
+        """u16 distances to destination d (host LRU)."""
+        return np.asarray(self.sp.host_row(d)[0]).view(np.uint16)
+
+    def sp_views(self):
+        """(dist, nh) read views over the whole shortest pool (Wide)."""
+        a = self.sp.tables()
+        if a is None:
+            return None, None
+        return Wide(a[0], "u16raw"), Wide(a[1], "u16" if self.V <= 0xFFFF else "int")
+
+    def sp_host(self, slots):
+        """(dist u16, nh int64) numpy rows of pool slots."""
+        a = self.sp.tables()
+        d = _host(_take(a[0], slots)).view(np.uint16)
+        nh = _host(_take(a[1], slots))
+        return d, (_u16(nh) if self.V <= 0xFFFF else nh.astype(np.int64))
+
+    # -- graph changes ---------------------------------------------------
+    def retarget(self, export, diff):
+        """Follow a link change over the same vertex set: drop the rows
+        ``diff`` can alter (tests run where the tables live), keep the rest.
+        Returns False when the compact layout no longer fits the new graph
+        (the caller starts a new cache)."""
+        from .incremental import dfs_rows_affected, sp_rows_affected
+        if tree_layout(export.csr) != self.layout:
+            return False
+        self.export = export
+        if self.dfs.row:
+            par, hop = self.dfs_parent_hops()
+            verts = self.dfs.slot_vertices()
+            hit = np.asarray(dfs_rows_affected(par, hop, verts, diff), bool) & (verts >= 0)
+            self.dfs.drop(verts[hit].tolist())
+            self.rows_inherited += len(self.dfs.row)
+        if self.sp.row:
+            dist, nh = self.sp_views()
+            verts = self.sp.slot_vertices()
+            hit = np.asarray(sp_rows_affected(dist, nh, diff), bool) & (verts >= 0)
+            self.sp.drop(verts[hit].tolist())
+            self.rows_inherited += len(self.sp.row)
+        self.dfs.host.clear()
+        self.sp.host.clear()
+        return True
+
+    # -- filling ---------------------------------------------------------
     def _rows(self, store, compute, wanted, batch):
-        """Ensure the rows of ``wanted`` (and as many of ``batch`` as the budget
-        allows) exist; return the merged tables."""
+        """Ensure the rows of ``wanted`` (and as many of ``batch`` as the
+        budget allows) exist; return the pool tables."""
         wanted = list(dict.fromkeys(int(v) for v in wanted))
         missing = [v for v in wanted if v not in store]
         miss = set(missing)
         extra = [int(v) for v in batch if int(v) not in store and int(v) not in miss] \
             if batch else []
+        for v in wanted:                       # recently used
+            if v in store.lru:
+                store.lru.move_to_end(v)
         if missing or extra:
             cap = store.cap()
             room = cap - len(store) - len(missing)
             extra = extra[:max(0, room)]
             todo = missing + extra
             store.make_room(len(todo), set(wanted))
-            tabs = compute(np.asarray(todo, np.int32))
+            for i in range(0, len(todo), COMPUTE_ROWS):
+                part = todo[i:i + COMPUTE_ROWS]
+                store.add(part, compute(np.asarray(part, np.int32)))
             self.rows_computed += len(todo)
-            store.add(todo, tabs)
         return store.tables()
 
+    def _dfs_compute(self, engine, srcs):
+        par, prt, hop = engine.dfs_tables(self.export, srcs)
+        if self.layout == INT32:
+            return par, prt, hop
+        tree = engine.pack_trees(self.export, par, prt, self.layout)
+        if _is_np(hop):
+            return tree, hop.astype(_hops_dtype(self.V))
+        return tree, hop.to(getattr(_torch(), _hops_dtype(self.V)))
+
+    def _sp_compute(self, engine, dsts):
+        dist, nh, _ = engine.shortest_tables(self.export, dsts)
+        dt = _nh_dtype(self.V)
+        if _is_np(dist):
+            return dist.view(np.int16), nh.astype(dt)
+        return dist, nh.to(getattr(_torch(), dt))
+
     def dfs_rows(self, engine, wanted, batch=()):
-        return self._rows(self.dfs, lambda s: engine.dfs_tables(self.export, s),
-                          wanted, batch)
+        return self._rows(self.dfs, lambda s: self._dfs_compute(engine, s), wanted, batch)
 
     def sp_rows(self, engine, wanted, batch=()):
-        return self._rows(self.sp, lambda d: engine.shortest_tables(self.export, d),
-                          wanted, batch)
+        return self._rows(self.sp, lambda d: self._sp_compute(engine, d), wanted, batch)
 
 
 def tree_path(parent_row, s, d):
@@ -402,8 +688,10 @@ def shortest_paths_lex(row_ptr, col, dist_row, s, d):
     order _find_routes_bfs returns them, topology_db.py:95-122): walk the
     shortest-path DAG (dist_row = hops to d) taking successors ascending."""
     INF = _native.DIST_INF
-    dist_row = np.asarray(dist_row).view(np.uint16) if np.asarray(dist_row).dtype == np.int16 \
-        else dist_row
+    dist_row = np.asarray(dist_row)
+    if dist_row.dtype == np.int16:
+        dist_row = dist_row.view(np.uint16)
+    dist_row = np.where(dist_row < 0, INF, dist_row)
     if int(dist_row[s]) == INF:
         return []
     out = []

@@ -8,7 +8,16 @@ entries (``tests/test_topologydb.py:30-61``, :74, :103).  Device tables are
 only valid for the graph they were computed on, so the drop-in stores the
 three dicts as :class:`TrackedDict` objects (plain ``dict`` subclasses) whose
 every mutation, including on the nested ``links[src]`` dicts, bumps a
-version counter the route cache compares against.
+version counter the route cache compares against -- and appends an entry to
+a change journal.
+
+Ryu delivers one event per change (``sdnmpi/topology.py:184-202``), so the
+export follows the journal instead of rebuilding from the dicts: a host on
+a known switch changes no CSR row at all, a link event patches one CSR row
+(:func:`update_export`).  Only a change of the vertex set (a new datapath, a
+switch losing its last link / host / switch entry), a whole-dict
+assignment, or a journal longer than ``JOURNAL_CAP`` entries re-exports from
+scratch (:func:`export_graph`).
 
 Limits of the tracking (documented in DESIGN.md): mutating an attribute of a
 Link/Host object in place (``link.src.port_no = ...``), or mutating a plain
@@ -20,71 +29,128 @@ import numpy as np
 
 from .topologies import CSR, build_csr
 
-__all__ = ["Versions", "TrackedDict", "export_graph", "GraphExport"]
+__all__ = ["Versions", "TrackedDict", "export_graph", "update_export", "GraphExport",
+           "JOURNAL_CAP"]
+
+JOURNAL_CAP = 1 << 16          # journal entries kept before falling back to a full export
 
 
 class Versions(object):
-    """Mutation counters of one TopologyDB's three dicts."""
+    """Mutation counters of one TopologyDB's three dicts, and the journal of
+    changes since the last export (``None``: re-export from the dicts)."""
 
-    __slots__ = ("links", "switches", "hosts")
+    __slots__ = ("links", "switches", "hosts", "journal")
 
     def __init__(self):
         self.links = 0
         self.switches = 0
         self.hosts = 0
+        self.journal = None
 
     def key(self):
         return (self.links, self.switches, self.hosts)
 
+    def log(self, entry):
+        j = self.journal
+        if j is not None:
+            if len(j) >= JOURNAL_CAP:
+                self.journal = None
+            else:
+                j.append(entry)
+
+    def take(self):
+        """The journal since the last take (None if it cannot be followed),
+        and a fresh one."""
+        j = self.journal
+        self.journal = []
+        return j
+
 
 class TrackedDict(dict):
-    """dict that bumps ``versions.<field>`` on every mutation.
+    """dict that bumps ``versions.<field>`` on every mutation and journals it.
 
     With ``nested=True`` (the outer ``links`` dict) dict values are stored as
-    TrackedDicts reporting to the same counter.
+    TrackedDicts reporting to the same counter, each knowing its key
+    (``owner``): a change inside ``links[u]`` journals ("edge", u, v), a
+    change of ``links[u]`` itself ("row", u); ``switches`` journals ("sw",
+    dpid), ``hosts`` ("host", mac, old Host, new Host).  Bulk operations
+    (whole-dict assignment, ``update``, ``clear``, ``popitem`` on the outer
+    dicts) void the journal.
     """
 
-    __slots__ = ("_versions", "_field", "_nested")
+    __slots__ = ("_versions", "_field", "_nested", "_owner")
 
-    def __init__(self, versions, field, data=None, nested=False):
+    def __init__(self, versions, field, data=None, nested=False, owner=None):
         dict.__init__(self)
         self._versions = versions
         self._field = field
         self._nested = nested
+        self._owner = owner
         if data:
             for k, v in dict(data).items():
-                dict.__setitem__(self, k, self._wrap(v))
+                dict.__setitem__(self, k, self._wrap(k, v))
+        if owner is None:              # a whole dict: the journal cannot follow
+            versions.journal = None
         self._bump()
 
     def _bump(self):
         setattr(self._versions, self._field, getattr(self._versions, self._field) + 1)
 
-    def _wrap(self, v):
+    def _wrap(self, k, v):
         if self._nested and isinstance(v, dict) and not (
-                isinstance(v, TrackedDict) and v._versions is self._versions):
-            return TrackedDict(self._versions, self._field, v)
+                isinstance(v, TrackedDict) and v._versions is self._versions and v._owner == k):
+            return TrackedDict(self._versions, self._field, v, owner=k)
         return v
 
+    def _note(self, k, old=None, new=None):
+        f = self._field
+        if f == "links":
+            if self._owner is None:
+                self._versions.log(("row", k))
+            else:
+                self._versions.log(("edge", self._owner, k))
+        elif f == "switches":
+            self._versions.log(("sw", k))
+        else:
+            self._versions.log(("host", k, old, new))
+
+    def _note_all(self):
+        if self._owner is None:
+            self._versions.journal = None
+        else:                          # an inner links dict: its row
+            self._versions.log(("row", self._owner))
+
     def __setitem__(self, k, v):
-        dict.__setitem__(self, k, self._wrap(v))
+        old = dict.get(self, k)
+        v = self._wrap(k, v)
+        dict.__setitem__(self, k, v)
+        self._note(k, old, v)
         self._bump()
 
     def __delitem__(self, k):
+        old = dict.__getitem__(self, k)
         dict.__delitem__(self, k)
+        self._note(k, old, None)
         self._bump()
 
-    def pop(self, *a):
-        r = dict.pop(self, *a)
+    def pop(self, k, *a):
+        had = k in self
+        old = dict.get(self, k)
+        r = dict.pop(self, k, *a)
+        if had:
+            self._note(k, old, None)
         self._bump()
         return r
 
     def popitem(self):
         r = dict.popitem(self)
+        self._note_all()
         self._bump()
         return r
 
     def clear(self):
         dict.clear(self)
+        self._note_all()
         self._bump()
 
     def setdefault(self, k, default=None):
@@ -94,7 +160,8 @@ class TrackedDict(dict):
 
     def update(self, *a, **kw):
         for k, v in dict(*a, **kw).items():
-            dict.__setitem__(self, k, self._wrap(v))
+            dict.__setitem__(self, k, self._wrap(k, v))
+        self._note_all()
         self._bump()
 
     def __ior__(self, other):
@@ -106,31 +173,222 @@ class TrackedDict(dict):
 
 
 class GraphExport(object):
-    """CSR of the switch graph plus the version key it was built from."""
+    """CSR of the switch graph, the version key it was built from, and the
+    per-vertex bookkeeping that lets journaled changes patch it: in-degree,
+    switch flag and host count per dense vertex (a vertex belongs to the
+    export while any of out-degree, in-degree, switch flag, hosts is set)."""
 
-    __slots__ = ("csr", "key", "index")
+    __slots__ = ("csr", "key", "index", "in_deg", "is_switch", "host_count", "_hv", "dport")
 
-    def __init__(self, csr, key):
+    def __init__(self, csr, key, index=None):
         self.csr = csr
         self.key = key
-        self.index = {int(d): i for i, d in enumerate(csr.dpids.tolist())}
+        self.index = index if index is not None else \
+            {int(d): i for i, d in enumerate(csr.dpids.tolist())}
+        self.in_deg = None
+        self.is_switch = None
+        self.host_count = None
+        self._hv = None
+        self.dport = None          # link.dst.port_no per CSR entry (flood helper)
+
+    def link_ends(self):
+        """Sorted uint64 keys (dense id << 32 | port_no) of both ends of every
+        link: the ports the reference's _is_edge_port compares with
+        (sdnmpi/topology.py:150-155)."""
+        c = self.csr
+        src = np.repeat(np.arange(c.V, dtype=np.uint64), np.diff(c.row_ptr.astype(np.int64)))
+        a = (src << np.uint64(32)) | (c.port.astype(np.int64).astype(np.uint64) &
+                                      np.uint64(0xFFFFFFFF))
+        b = (c.col.astype(np.uint64) << np.uint64(32)) | \
+            (self.dport.astype(np.int64).astype(np.uint64) & np.uint64(0xFFFFFFFF))
+        return np.sort(np.concatenate([a, b]))
+
+    def host_vertices(self):
+        """Ascending dense ids of the switches hosts attach to."""
+        if self._hv is None:
+            self._hv = np.nonzero(self.host_count)[0].tolist()
+        return self._hv
 
 
 def export_graph(links, switches, hosts, key=None):
     """Dense CSR of ``links`` (vertex set = link endpoints, switches and host
     dpids, ascending dpid order; row order = ``sorted(links[u])``, the
     reference's neighbour order, topology_db.py:76; port = ``link.src.port_no``,
-    :130)."""
-    src, dst, sport = [], [], []
+    :130), with the bookkeeping of :class:`GraphExport`."""
+    src, dst, sport, dport = [], [], [], []
     for u, nbrs in links.items():
         for v, link in nbrs.items():
             src.append(u)
             dst.append(v)
             sport.append(int(link.src.port_no))
+            dport.append(int(link.dst.port_no))
+    hdp = [h.port.dpid for h in hosts.values()]
     extra = list(switches.keys())
-    extra.extend(h.port.dpid for h in hosts.values())
+    extra.extend(hdp)
     csr = build_csr(src, dst, np.asarray(sport, np.int64), extra_vertices=extra)
-    return GraphExport(csr, key)
+    ex = GraphExport(csr, key)
+    V = csr.V
+    # dict rows hold each (src, dst) once, so build_csr's order is the sort
+    # by (src id, dst id): the destination ports follow it
+    if src:
+        key2 = csr.index_of(src).astype(np.int64) * V + csr.index_of(dst)
+        ex.dport = np.asarray(dport, np.int64)[np.argsort(key2, kind="stable")].astype(np.int32)
+    else:
+        ex.dport = np.zeros(0, np.int32)
+    ex.in_deg = np.bincount(csr.col, minlength=V).astype(np.int64) if V else np.zeros(0, np.int64)
+    ex.is_switch = np.zeros(V, bool)
+    if switches:
+        ex.is_switch[csr.index_of(list(switches.keys()))] = True
+    ex.host_count = np.bincount(csr.index_of(hdp), minlength=V).astype(np.int64) if hdp \
+        else np.zeros(V, np.int64)
+    return ex
+
+
+def update_export(ex, journal, links, switches, hosts, key):
+    """Follow the journaled changes from export ``ex``.
+
+    Returns ``(export, diff)``: ``export`` is ``ex`` itself, updated in place,
+    when no CSR row changed (hosts or switch entries only; ``diff`` None), or
+    a new export sharing ``ex``'s vertex set with the changed rows patched
+    and ``diff`` their :class:`~sdnmpi_amd.incremental.EdgeDiff`.  Returns
+    None when the vertex set may have changed (the caller re-exports).  Cost:
+    O(changed rows) Python plus O(V + E) numpy copies when a row changes.
+    """
+    from .incremental import EdgeDiff
+    idx = ex.index
+    csr = ex.csr
+    rows, sws, hents = set(), set(), []
+    for e in journal:
+        t = e[0]
+        if t == "edge" or t == "row":
+            rows.add(e[1])
+        elif t == "sw":
+            sws.add(e[1])
+        else:
+            hents.append(e)
+    touched = []
+    hc = ex.host_count
+    if hents:
+        hc = hc.copy()
+        for _, _, old, new in hents:
+            if old is not None:
+                i = idx.get(old.port.dpid)
+                if i is None:
+                    return None
+                hc[i] -= 1
+                touched.append(i)
+            if new is not None:
+                i = idx.get(new.port.dpid)
+                if i is None:
+                    return None                      # a host on a new datapath
+                hc[i] += 1
+    sw = ex.is_switch
+    if sws:
+        sw = sw.copy()
+        for d in sws:
+            i = idx.get(d)
+            now = d in switches
+            if i is None:
+                if now:
+                    return None                      # a new switch
+                continue
+            sw[i] = now
+            touched.append(i)
+    # link rows: compare each touched row with its current dict
+    rp = csr.row_ptr
+    in_deg = ex.in_deg
+    new_rows = {}
+    rem_u, rem_v, add_u, add_v, prt_u, prt_v = [], [], [], [], [], []
+    for u in rows:
+        i = idx.get(u)
+        nb = links.get(u)
+        if i is None:
+            if nb:
+                return None                          # links out of a new datapath
+            continue
+        ids, ports, dports = [], [], []
+        for v, link in (nb or {}).items():
+            j = idx.get(v)
+            if j is None:
+                return None                          # a link to a new datapath
+            ids.append(j)
+            ports.append(int(link.src.port_no))
+            dports.append(int(link.dst.port_no))
+        order = np.argsort(np.asarray(ids, np.int64), kind="stable")
+        ncol = np.asarray(ids, np.int32)[order]
+        nport = np.asarray(ports, np.int64)[order]
+        ndport = np.asarray(dports, np.int64)[order].astype(np.int32)
+        ocol = csr.col[rp[i]:rp[i + 1]]
+        oport = csr.port[rp[i]:rp[i + 1]]
+        if ncol.shape == ocol.shape and np.array_equal(ncol, ocol) and \
+                np.array_equal(nport, oport) and \
+                np.array_equal(ndport, ex.dport[rp[i]:rp[i + 1]]):
+            continue
+        if nport.size and (nport.max() > 0x7FFFFFFF or nport.min() < -0x80000000):
+            raise ValueError("port numbers must fit in int32")
+        common, io, inn = np.intersect1d(ocol, ncol, assume_unique=True, return_indices=True)
+        gone = np.setdiff1d(ocol, ncol, assume_unique=True)
+        came = np.setdiff1d(ncol, ocol, assume_unique=True)
+        rep = common[oport[io] != nport[inn]]
+        if in_deg is ex.in_deg:
+            in_deg = in_deg.copy()
+        np.subtract.at(in_deg, gone, 1)
+        np.add.at(in_deg, came, 1)
+        rem_u += [i] * gone.size
+        rem_v += gone.tolist()
+        add_u += [i] * came.size
+        add_v += came.tolist()
+        prt_u += [i] * rep.size
+        prt_v += rep.tolist()
+        touched.append(i)
+        touched.extend(gone.tolist())
+        new_rows[i] = (ncol, nport.astype(np.int32), ndport)
+    # the vertex set must not shrink
+    if touched:
+        t = np.asarray(touched, np.int64)
+        out_deg = np.diff(rp)[t]
+        for i, r in new_rows.items():
+            out_deg[t == i] = r[0].size
+        member = (out_deg > 0) | (in_deg[t] > 0) | sw[t] | (hc[t] > 0)
+        if not member.all():
+            return None
+    if not new_rows:
+        ex.key = key
+        if hc is not ex.host_count:
+            ex.host_count = hc
+            ex._hv = None
+        ex.is_switch = sw
+        return ex, None
+    # patched CSR: unchanged spans copied between the new rows
+    deg = np.diff(rp).astype(np.int64)
+    for i, r in new_rows.items():
+        deg[i] = r[0].size
+    nrp = np.zeros(csr.V + 1, np.int64)
+    np.cumsum(deg, out=nrp[1:])
+    cols, ports, dps, prev = [], [], [], 0
+    for i in sorted(new_rows):
+        cols.append(csr.col[rp[prev]:rp[i]])
+        ports.append(csr.port[rp[prev]:rp[i]])
+        dps.append(ex.dport[rp[prev]:rp[i]])
+        c, p, q = new_rows[i]
+        cols.append(c)
+        ports.append(p)
+        dps.append(q)
+        prev = i + 1
+    cols.append(csr.col[rp[prev]:])
+    ports.append(csr.port[rp[prev]:])
+    dps.append(ex.dport[rp[prev]:])
+    ncsr = CSR(csr.dpids, nrp, np.concatenate(cols), np.concatenate(ports))
+    new = GraphExport(ncsr, key, index=idx)
+    new.dport = np.concatenate(dps)
+    new.in_deg = in_deg
+    new.is_switch = sw
+    new.host_count = hc
+    new._hv = ex._hv if hc is ex.host_count else None
+
+    def pair(a, b):
+        return np.asarray(a, np.int64), np.asarray(b, np.int64)
+    return new, EdgeDiff(pair(rem_u, rem_v), pair(add_u, add_v), pair(prt_u, prt_v))
 
 
 def empty_csr():

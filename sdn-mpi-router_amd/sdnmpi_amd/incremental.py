@@ -132,6 +132,7 @@ class _TorchNS(object):
 
 
 def _ns(a):
+    a = getattr(a, "arr", a)           # engine.Wide: a decoding view of a compact table
     return _NumpyNS() if isinstance(a, np.ndarray) else _TorchNS(a.device)
 
 

@@ -12,19 +12,22 @@ What changes is how a route is found.  Instead of one Python stack search
 per (src, dst) pair, the switch graph is exported as a CSR and the GPU
 computes whole tables -- per source the tree of the reference's LIFO
 traversal (every destination at once), per destination the hop distances
-of the shortest-route mode -- which are cached until the dicts change and
-walked per query.  ``route_tables()`` / ``find_routes()`` expose the batched
-all-pairs form the MPI router needs.
+of the shortest-route mode -- which are cached and walked per query.  A
+topology event patches the export (one CSR row per link event, nothing for a
+host on a known switch) and drops only the cached rows it can alter.
+``route_tables()`` / ``find_routes()`` expose the batched all-pairs form the
+MPI router needs.
 
 There is no CPU fallback: without ``libsdnroute.so`` or a gfx950 device the
 first route query raises (``sdnmpi_amd._native.NativeUnavailable`` /
-``SdnrError``).
+``SdnrError``), and so does the first flood-port query (``is_edge_port`` /
+``edge_ports`` / ``broadcast_ports``: their bulk pass is sdnr_edge_ports).
 """
 
 import numpy as np
 
 from ..engine import RouteEngine, TableCache, _host, _take, shortest_paths_lex, tree_path
-from ..graph import TrackedDict, Versions, export_graph
+from ..graph import TrackedDict, Versions, export_graph, update_export
 from ..incremental import edge_diff
 
 try:   # the reference takes OFPP_LOCAL from Ryu's OpenFlow 1.0 module (:5)
@@ -66,8 +69,7 @@ class TopologyDB(object):
         self._incremental = incremental
         self._export = None
         self._cache = None
-        self._hv = (None, None)          # (version key, host vertices)
-        self._em = (None, None)          # (links/switches version, edge-port state)
+        self._em = (None, None, None)    # (links/switches version, edge-port state, export)
         # Switch DPID -> Switch; src DPID -> dst DPID -> Link; MAC -> Host
         self.switches = {}
         self.links = {}
@@ -138,29 +140,39 @@ class TopologyDB(object):
         return self._engine
 
     def graph(self):
-        """Current CSR export (re-exported after any dict mutation)."""
+        """Current CSR export.  Mutations since the last export are followed
+        from the dicts' journal (graph.update_export: O(changed rows)); a
+        vertex-set change or a whole-dict assignment re-exports."""
         key = self._versions.key()
         ex = self._export
-        if ex is None or ex.key != key:
+        if ex is not None and ex.key == key:
+            return ex
+        journal = self._versions.take()
+        res = None
+        if ex is not None and journal is not None:
+            res = update_export(ex, journal, self.links, self.switches, self.hosts, key)
+        if res is None:
             new = export_graph(self.links, self.switches, self.hosts, key)
             if ex is not None and _same_graph(ex.csr, new.csr):
-                ex.key = key             # only host ports / MACs changed
-            else:
-                old = self._cache
-                self._export = ex = new
-                self._cache = TableCache(new, self._budget)
-                if self._incremental and old is not None:
-                    diff = edge_diff(old.export.csr, new.csr)
-                    if diff is not None:
-                        self._cache.inherit(old, diff)
-        return ex
+                # same links over the same vertex set (e.g. hosts moved)
+                ex.key = key
+                ex.host_count, ex.is_switch, ex._hv = new.host_count, new.is_switch, None
+                ex.dport = new.dport
+                return ex
+            diff = edge_diff(ex.csr, new.csr) if ex is not None else None
+        else:
+            new, diff = res
+            if new is ex:                # hosts / switch entries only
+                return ex
+        old = self._cache
+        self._export = new
+        if not (self._incremental and old is not None and diff is not None and
+                old.retarget(new, diff)):
+            self._cache = TableCache(new, self._budget)
+        return new
 
     def _host_vertices(self, ex):
-        key = self._versions.key()
-        if self._hv[0] != key:
-            idx = ex.index
-            self._hv = (key, sorted({idx[h.port.dpid] for h in self.hosts.values()}))
-        return self._hv[1]
+        return ex.host_vertices()
 
     def _dfs(self, ex, s):
         """(parent, port) host rows of source s (one row copied back from
@@ -169,15 +181,14 @@ class TopologyDB(object):
         if s not in c.dfs:
             batch = self._host_vertices(ex) if self._batch else ()
             c.dfs_rows(self.engine, [s], batch)
-        row = c.dfs.host_row(s)
-        return row[0], row[1]
+        return c.dfs_host_row(s)
 
     def _dist(self, ex, d):
         c = self._cache
         if d not in c.sp:
             batch = self._host_vertices(ex) if self._batch else ()
             c.sp_rows(self.engine, [d], batch)
-        return c.sp.host_row(d)[0]
+        return c.sp_dist_host_row(d)
 
     # -- route lookup (topology_db.py:124-188) ---------------------------
     def _mac_to_int(self, mac):
@@ -239,18 +250,14 @@ class TopologyDB(object):
         """(sorted link-end keys, {(dpid, port_no): is_edge} of every switch
         port) for the current links/switches, from one device pass
         (sdnr_edge_ports) per version instead of the reference's scan over
-        every link per port.  Keys: dense switch id << 32 | port_no."""
+        every link per port.  Keys: dense switch id << 32 | port_no; the link
+        ends come from the export (both ends of every CSR entry), keyed with
+        the same dense ids (the cache is tied to the export object)."""
         key = (self._versions.links, self._versions.switches)
-        if self._em[0] != key:
-            idx = self.graph().index
-            ends = set()
-            for nb in self.links.values():
-                for lk in nb.values():
-                    for p in (lk.src, lk.dst):
-                        d = idx.get(p.dpid)
-                        if d is not None:
-                            ends.add((d << 32) | (int(p.port_no) & 0xFFFFFFFF))
-            ends = np.asarray(sorted(ends), np.uint64)
+        ex = self.graph()
+        if self._em[0] != key or self._em[2] is not ex:
+            idx = ex.index
+            ends = ex.link_ends()
             ports, keys = [], []
             for sw in self.switches.values():
                 for p in getattr(sw, "ports", ()):
@@ -259,12 +266,14 @@ class TopologyDB(object):
                         ports.append((p.dpid, p.port_no))
                         keys.append((d << 32) | (int(p.port_no) & 0xFFFFFFFF))
             mask = self.engine.edge_ports(ends, np.asarray(keys, np.uint64)) if keys else []
-            self._em = (key, (ends, dict(zip(ports, (bool(m) for m in mask)))))
+            self._em = (key, (ends, dict(zip(ports, (bool(m) for m in mask)))), ex)
         return self._em[1]
 
     def is_edge_port(self, port):
         """``TopologyManager._is_edge_port`` (reference sdnmpi/topology.py:
-        150-155): the port is neither end of any link."""
+        150-155): the port is neither end of any link.  Ports of the
+        switches' port lists come from the device pass; any other port is
+        one binary search in the sorted link ends."""
         ends, known = self._edge_state()
         hit = known.get((port.dpid, port.port_no))
         if hit is not None:
@@ -272,8 +281,9 @@ class TopologyDB(object):
         d = self.graph().index.get(port.dpid)
         if d is None:                     # not a switch of the graph: no link end
             return True
-        k = np.asarray([(d << 32) | (int(port.port_no) & 0xFFFFFFFF)], np.uint64)
-        return bool(self.engine.edge_ports(ends, k)[0])
+        k = np.uint64((d << 32) | (int(port.port_no) & 0xFFFFFFFF))
+        i = int(np.searchsorted(ends, k))
+        return not (i < ends.shape[0] and ends[i] == k)
 
     def edge_ports(self, switch, in_port=None):
         """The ports ``_do_broadcast`` floods on ``switch`` (topology.py:
@@ -313,12 +323,16 @@ class TopologyDB(object):
         store = c.dfs if mode == "dfs" else c.sp
         get = c.dfs_rows if mode == "dfs" else c.sp_rows
         parts = []                    # host copies, a budget's worth of rows at a time
-        step = store.cap() if store.row_bytes else len(hv)
-        for i in range(0, len(hv), max(1, step)):
-            chunk = hv[i:i + max(1, step)]
-            tabs = get(self.engine, chunk)
+        step = max(1, store.cap())
+        for i in range(0, len(hv), step):
+            chunk = hv[i:i + step]
+            get(self.engine, chunk)
             idx = np.asarray([store.row[v] for v in chunk], np.int64)
-            parts.append(tuple(_host(_take(a, idx)) for a in tabs))
+            if mode == "dfs":
+                parts.append(tuple(_host(a).astype(np.int32) for a in c.dfs_int32(idx, self.engine)))
+            else:
+                d, nh = c.sp_host(idx)
+                parts.append((d, nh.astype(np.int32), _edge_ports(ex.csr, nh)))
         V = ex.csr.V
         empty = (np.zeros((0, V), np.int32), np.zeros((0, V), np.int32),
                  np.zeros((0, V), np.int32)) if mode == "dfs" else \
@@ -327,9 +341,7 @@ class TopologyDB(object):
         if mode == "dfs":
             return {"sources": np.asarray(hv, np.int32), "parent": cols[0],
                     "port": cols[1], "hops": cols[2], "dpids": ex.csr.dpids}
-        dist = cols[0].view(np.uint16) if cols[0] is not None and cols[0].dtype == np.int16 \
-            else cols[0]
-        return {"destinations": np.asarray(hv, np.int32), "dist": dist,
+        return {"destinations": np.asarray(hv, np.int32), "dist": cols[0],
                 "nh": cols[1], "nh_port": cols[2], "dpids": ex.csr.dpids}
 
     def _find_routes_multiple(self, pairs):
@@ -403,10 +415,13 @@ class TopologyDB(object):
         pieces = []                   # (pair ids, offsets, switches, ports) per source chunk
         for c0 in range(0, len(want), step):        # a budget's worth of sources at a time
             chunk = want[c0:c0 + step]
-            tabs = c.dfs_rows(self.engine, chunk, batch if c0 == 0 else ())
+            c.dfs_rows(self.engine, chunk, batch if c0 == 0 else ())
             mine = ok[np.isin(sv[ok], np.asarray(chunk, np.int64))]
-            rows = np.asarray([c.dfs_row[v] for v in sv[mine].tolist()], np.int32)
-            o, sw, hp = self.engine.expand(ex, tabs, rows, dv[mine], last[mine])
+            slots = np.asarray([c.dfs_row[v] for v in sv[mine].tolist()], np.int64)
+            # only the rows these pairs use are decoded for the expansion
+            urows, inv = np.unique(slots, return_inverse=True)
+            tabs = c.dfs_int32(urows, self.engine)
+            o, sw, hp = self.engine.expand(ex, tabs, inv, dv[mine], last[mine])
             lens[mine] = np.diff(o)
             pieces.append((mine, o, sw, hp))
         np.cumsum(lens, out=off[1:])
@@ -446,6 +461,22 @@ class TopologyDB(object):
             if len(want) < self._cache.dfs.cap():
                 self._cache.dfs_rows(self.engine, sorted(want), self._host_vertices(ex))
         return [self.find_route(a, b, multiple) for a, b in pairs]
+
+
+def _edge_ports(csr, nh):
+    """links[x][nh[r, x]].src.port_no for every entry (-1 where nh < 0): the
+    next hops' ports, looked up in the CSR."""
+    V = csr.V
+    rp = np.asarray(csr.row_ptr, np.int64)
+    keys = np.repeat(np.arange(V, dtype=np.int64), np.diff(rp)) * V + \
+        np.asarray(csr.col, np.int64)
+    x = np.broadcast_to(np.arange(V, dtype=np.int64), nh.shape)
+    ok = nh >= 0
+    e = np.searchsorted(keys, np.where(ok, x * V + nh, 0))
+    e = np.minimum(e, max(keys.shape[0] - 1, 0))
+    if keys.shape[0] == 0:
+        return np.full(nh.shape, -1, np.int32)
+    return np.where(ok, np.asarray(csr.port, np.int32)[e], -1).astype(np.int32)
 
 
 def _same_graph(a, b):

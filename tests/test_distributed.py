@@ -145,6 +145,17 @@ def _rccl_worker(port, q):
             D.all_gather_rows_async(loc, out).wait()
             torch.cuda.synchronize()
             ok.append(bool(torch.equal(out, loc)))
+        # sharded_route_tables on the nccl backend over a subgroup: the shard
+        # travels as a device tensor, the gather uses the group passed in
+        import numpy as np
+        from sdnmpi_amd import topologies as T
+        from sdnmpi_amd.util.topology_db import TopologyDB
+        sub = dist.new_group([0])
+        db = T.fat_tree(4).populate(TopologyDB())
+        for mode in ("dfs", "shortest"):
+            got = D.sharded_route_tables(db, mode, group=sub)
+            want = db.route_tables(mode)
+            ok.append(all(np.array_equal(got[k], want[k]) for k in want))
         dist.destroy_process_group()
         q.put(ok)
     except Exception as e:   # noqa: BLE001 -- reported to the parent
@@ -159,4 +170,4 @@ def test_rccl_all_gather_table_dtypes():
     p.start()
     res = q.get(timeout=240)
     p.join(60)
-    assert res == [True, True], res
+    assert res == [True, True, True, True], res

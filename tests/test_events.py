@@ -1,0 +1,199 @@
+"""Topology events are O(change) (reference
+sdnmpi/topology.py:184-202 -> topology_db.py:20-42): the drop-in follows the
+dicts' change journal instead of re-exporting the CSR (graph.update_export),
+and the table cache keeps the rows a link change cannot alter in place.
+
+* the journaled export equals a from-scratch export after every event of
+  random event sequences, and takes the incremental path whenever the
+  vertex set is unchanged;
+* routes after every event equal the reference semantics (oracle restatement
+  of _find_route_dfs / _find_routes_bfs on the mutated dicts);
+* Jellyfish 100k: one add_host + find_route and one delete_link +
+  find_route each spend <= 50 ms in host code (was 3.0 s: a Python
+  re-export of 1.6 M links per event).  CPU only (the oracle-backed engine
+  double; its compute time is excluded)."""
+import time
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from sdnmpi_amd import topologies as T
+from sdnmpi_amd.graph import export_graph
+from sdnmpi_amd.objects import Host, Link, Port, Switch
+from sdnmpi_amd.util.topology_db import TopologyDB
+from test_topologydb_dropin import _FakeEngine
+
+
+def _full(db):
+    return export_graph(db.links, db.switches, db.hosts)
+
+
+def _same(ex, ref):
+    c, r = ex.csr, ref.csr
+    assert np.array_equal(c.dpids, r.dpids)
+    assert np.array_equal(c.row_ptr, r.row_ptr)
+    assert np.array_equal(c.col, r.col)
+    assert np.array_equal(c.port, r.port)
+    assert ex.host_vertices() == ref.host_vertices()
+    assert np.array_equal(ex.in_deg, ref.in_deg)
+    assert np.array_equal(ex.is_switch, ref.is_switch)
+    assert np.array_equal(ex.host_count, ref.host_count)
+
+
+def _events(db, rng, fabric_dpids, nxt):
+    """One random mutation of the kinds Ryu and the reference tests make."""
+    links = [(u, v) for u, nb in db.links.items() for v in nb]
+    k = int(rng.integers(0, 11))
+    if k <= 2 and links:                                   # EventLinkDelete
+        u, v = links[int(rng.integers(len(links)))]
+        db.delete_link(db.links[u][v])
+        return "delete_link"
+    if k == 3:                                             # EventLinkAdd (known switches)
+        u, v = (int(x) for x in rng.choice(fabric_dpids, 2, replace=False))
+        db.add_link(Link(Port(u, int(rng.integers(1, 60))), Port(v, int(rng.integers(1, 60)))))
+        return "add_link"
+    if k == 4 and links:                                   # re-ported link
+        u, v = links[int(rng.integers(len(links)))]
+        db.links[u][v] = Link(Port(u, int(rng.integers(100, 200))), Port(v, 7))
+        return "report"
+    if k == 5:                                             # EventHostAdd / host moves
+        d = int(rng.choice(fabric_dpids))
+        db.add_host(Host("02:00:00:00:%02x:%02x" % (int(rng.integers(0, 4)),
+                                                     int(rng.integers(0, 256))), Port(d, 33)))
+        return "add_host"
+    if k == 6 and db.hosts:
+        mac = sorted(db.hosts)[int(rng.integers(len(db.hosts)))]
+        del db.hosts[mac]
+        return "del_host"
+    if k == 7:                                             # switch entry churn
+        d = int(rng.choice(fabric_dpids))
+        if d in db.switches:
+            db.delete_switch(db.switches[d])
+        else:
+            db.add_switch(Switch(d))
+        return "switch"
+    if k == 8:                                             # a new datapath
+        nxt[0] += 1
+        u = int(rng.choice(fabric_dpids))
+        db.add_link(Link(Port(nxt[0], 1), Port(u, 90)))
+        db.add_link(Link(Port(u, 90), Port(nxt[0], 1)))
+        fabric_dpids.append(nxt[0])
+        return "new_vertex"
+    if k == 9 and links:                                   # nested dict replaced
+        u = links[int(rng.integers(len(links)))][0]
+        row = dict(db.links[u])
+        if row:
+            row.pop(sorted(row)[0])
+        db.links[u] = row
+        return "row"
+    if links:                                              # a switch loses its rows
+        u = links[int(rng.integers(len(links)))][0]
+        db.links[u].clear()
+        return "clear_row"
+    return "none"
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_journaled_export_equals_full_export(seed):
+    rng = np.random.default_rng(seed)
+    fabric = T.fat_tree(4)
+    db = fabric.populate(TopologyDB())
+    db._engine = _FakeEngine()
+    dpids = [int(d) for d in fabric.csr().dpids]
+    nxt = [10 ** 6]
+    ex = db.graph()
+    incremental = 0
+    for _ in range(120):
+        kind = _events(db, rng, dpids, nxt)
+        new = db.graph()
+        _same(new, _full(db))
+        if kind in ("add_host", "report", "add_link") and new.index is ex.index:
+            incremental += 1
+        ex = new
+    assert incremental > 20
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_routes_after_every_event(seed):
+    rng = np.random.default_rng(50 + seed)
+    fabric = T.fat_tree(4)
+    db = fabric.populate(TopologyDB())
+    db._engine = _FakeEngine()
+    dpids = [int(d) for d in fabric.csr().dpids]
+    nxt = [10 ** 6]
+    for step in range(40):
+        _events(db, rng, dpids, nxt)
+        macs = sorted(db.hosts)
+        sample = [(macs[int(i)], macs[int(j)])
+                  for i, j in rng.integers(0, len(macs), (12, 2))] if macs else []
+        for a, b in sample:
+            assert db.find_route(a, b) == O.find_route_pair(db, a, b), step
+        for a, b in sample[:4]:
+            assert db.find_route(a, b, True) == O.find_routes_all_shortest(db, a, b), step
+
+
+def test_host_only_changes_keep_export_object():
+    fabric = T.fat_tree(4)
+    db = fabric.populate(TopologyDB())
+    db._engine = _FakeEngine()
+    macs = fabric.host_macs()
+    db.find_route(macs[0], macs[5])
+    ex, cache = db.graph(), db._cache
+    db.add_host(Host("02:00:00:00:aa:01", Port(int(fabric.host_dpid[3]), 40)))
+    del db.hosts[macs[7]]
+    assert db.graph() is ex and db._cache is cache
+    _same(ex, _full(db))
+
+
+class _TimedEngine(_FakeEngine):
+    """The engine double, with the time spent inside it."""
+
+    def __init__(self):
+        super(_TimedEngine, self).__init__()
+        self.spent = 0.0
+
+    def dfs_tables(self, *a, **k):
+        t = time.perf_counter()
+        try:
+            return super(_TimedEngine, self).dfs_tables(*a, **k)
+        finally:
+            self.spent += time.perf_counter() - t
+
+    def pack_trees(self, *a, **k):
+        t = time.perf_counter()
+        try:
+            return super(_TimedEngine, self).pack_trees(*a, **k)
+        finally:
+            self.spent += time.perf_counter() - t
+
+
+def test_jellyfish_events_are_o_change():
+    fabric = T.jellyfish(100000, 16, seed=1)
+    db = fabric.populate(TopologyDB(batch_sources=False))
+    eng = _TimedEngine()
+    db._engine = eng
+    macs = fabric.host_macs()
+    a, b = macs[0], macs[123]
+    assert db.find_route(a, b) == O.find_route_pair(db, a, b)      # full export (3 s), once
+
+    def host_ms(f):
+        s0 = eng.spent
+        t = time.perf_counter()
+        f()
+        return (time.perf_counter() - t - (eng.spent - s0)) * 1e3
+
+    # EventHostAdd on a known switch, then a query
+    new_mac = "02:00:00:00:bb:01"
+    ms_host = host_ms(lambda: (db.add_host(Host(new_mac, Port(int(fabric.host_dpid[5]), 2))),
+                               db.find_route(a, new_mac)))
+    assert db.find_route(a, new_mac) == O.find_route_pair(db, a, new_mac)
+    # EventLinkDelete of a link on the queried route, then a query
+    route = db.find_route(a, b)
+    u = route[0][0]
+    v = next(iter(db.links[u]))
+    ms_link = host_ms(lambda: (db.delete_link(db.links[u][v]), db.find_route(a, b)))
+    assert db.find_route(a, b) == O.find_route_pair(db, a, b)
+    print("host-code ms: add_host+find_route %.1f, delete_link+find_route %.1f" % (ms_host, ms_link))
+    assert ms_host <= 50.0, ms_host
+    assert ms_link <= 50.0, ms_link

@@ -156,6 +156,11 @@ class _FakeEngine(object):
         self.calls.append(("sp", export.key, tuple(int(x) for x in dsts)))
         return self.O.dest_tables(export.csr, dsts)
 
+    def pack_trees(self, export, parent, port, layout):
+        # host packing (test double of sdnr_tree_pack)
+        from sdnmpi_amd.engine import pack_host_tree
+        return pack_host_tree(parent, port, export.csr, layout)
+
     def ecmp(self, export, dist, rows, srcs):
         # host walk of the shortest-path DAG (test double only)
         from sdnmpi_amd.engine import shortest_paths_lex
@@ -254,16 +259,18 @@ def _link_failure_replay(db, fabric):
     a = int(dp[t["parent"][0][0]])     # vertex 0 = core 0
     ab = db.links[a][1]
     ba = db.links[1][a]
+    n0 = db._cache.rows_computed
     db.delete_link(ab)
     db.delete_link(ba)
     got = db.find_routes(pairs)
     assert got == [O.find_route_pair(db, a, b) for a, b in pairs]
     c = db._cache
-    assert 0 < c.rows_computed < hosts and c.rows_inherited > 0
+    assert 0 < c.rows_computed - n0 < hosts and c.rows_inherited > 0
+    n1 = c.rows_computed
     db.add_link(ab)
     db.add_link(ba)
     assert db.find_routes(pairs) == [O.find_route_pair(db, a, b) for a, b in pairs]
-    assert db._cache.rows_computed < hosts
+    assert db._cache.rows_computed - n1 < hosts
     # shortest mode keeps its rows across the change too
     sp = [db.find_route(a, b, True) for a, b in pairs[:40]]
     assert sp == [O.find_routes_all_shortest(db, a, b) for a, b in pairs[:40]]
@@ -446,20 +453,24 @@ def test_table_budget_eviction_fake_engine(budget_rows):
     sources -- and every answer still equals the reference semantics."""
     from oracle import oracle as O
     from sdnmpi_amd import topologies as T
+    from sdnmpi_amd.engine import dfs_row_bytes, sp_row_bytes
     fabric = T.fat_tree(4)
-    V = fabric.csr().V
-    db = fabric.populate(TopologyDB(table_budget=budget_rows * 3 * 4 * V))
+    csr = fabric.csr()
+    budget = budget_rows * dfs_row_bytes(csr)          # compact rows: 6 B per entry
+    assert dfs_row_bytes(csr) == 6 * csr.V and sp_row_bytes(csr) == 4 * csr.V
+    db = fabric.populate(TopologyDB(table_budget=budget))
     eng = _FakeEngine()
     db._engine = eng
     macs = fabric.host_macs()
     pairs = [(a, b) for a in macs for b in macs[::2]]
     assert db.find_routes(pairs) == [O.find_route_pair(db, a, b) for a, b in pairs]
     assert len(db._cache.dfs) <= budget_rows
+    assert db._cache.dfs.size <= budget_rows           # the pool never outgrows the budget
     for a, b in pairs[::7]:
         assert db.find_route(a, b) == O.find_route_pair(db, a, b)
     assert db.find_routes(pairs[:40], True) == \
         [O.find_routes_all_shortest(db, a, b) for a, b in pairs[:40]]
-    assert len(db._cache.sp) <= max(1, budget_rows * 3 * 4 * V // (10 * V))
+    assert len(db._cache.sp) <= max(1, budget // sp_row_bytes(csr))
     t = db.route_tables("dfs")
     po, to, ho = O.dfs_tables(fabric.csr(), t["sources"])
     np.testing.assert_array_equal(t["parent"], po)
