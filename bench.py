@@ -73,6 +73,10 @@ def parse():
                     help="dfs mode: skip the materialised flow-entry rate of every host pair")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0,
                     help="bound on the CPU baseline's work")
+    ap.add_argument("--assemble", choices=["all", "root"], default="all",
+                    help="N > 1: tables assembled on every rank (RCCL all-gather, default) "
+                         "or on rank 0 only (point-to-point receives into the root); the "
+                         "other form is measured beside it in the multi_gpu block")
     return ap.parse_args()
 
 
@@ -481,6 +485,106 @@ def main_apsp(args, world, rank, local, dev):
     ctx.close()
 
 
+def _max_min(x, dev):
+    """(max, min) of a float over the ranks."""
+    on = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+    a = torch.tensor([x], dtype=torch.float64, device=on)
+    b = torch.tensor([-x], dtype=torch.float64, device=on)
+    dist.all_reduce(a, op=dist.ReduceOp.MAX)
+    dist.all_reduce(b, op=dist.ReduceOp.MAX)
+    return float(a.item()), -float(b.item())
+
+
+def multi_gpu_extras(args, world, rank, local, dev, csr, srcs, per, packed, slots, kern_ms,
+                     ms_per_step, routes, step, drain, bufs, gathered, assemble):
+    """N > 1: what the step time is made of, and the other assembly forms.
+
+    kernel_ms_max / _min  the route kernel per rank (HIP events);
+    gather_ms             the table assembly alone (same tensors, no kernel);
+    overlap               share of the shorter of the two hidden under the
+                          other in the double-buffered step;
+    assemble_{all,root}   ms per step with the tables assembled on every rank
+                          (RCCL all-gather) / on rank 0 only (point-to-point);
+    single_process        ms per step of ONE process driving all N devices
+                          (sdnr_create_multi: shards on every device, rows
+                          peer-copied to device 0), measured by rank 0 while
+                          the other ranks wait."""
+    reps = max(2, args.steps)
+
+    def timed(fn):
+        drain()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        drain()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        return _max_min((time.perf_counter() - t0) / reps * 1e3, dev)[0]
+
+    def gather_only():
+        for t, g in zip(bufs[0], gathered[0]):
+            (D.all_gather_rows_async(t, g) if assemble[0] == "all"
+             else D.gather_rows_to_root(t, g)).wait()
+
+    kmax, kmin = _max_min(kern_ms, dev)
+    gather_ms = timed(gather_only)
+    other = "root" if args.assemble == "all" else "all"
+    assemble[0] = other
+    other_ms = timed(step)
+    assemble[0] = args.assemble
+    hidden = kmax + gather_ms - ms_per_step
+    res = {
+        "kernel_ms_max": kmax, "kernel_ms_min": kmin, "gather_ms": gather_ms,
+        "overlap": max(0.0, min(1.0, hidden / max(1e-9, min(kmax, gather_ms)))),
+        "assemble_" + args.assemble: {"ms_per_step": ms_per_step,
+                                      "value": routes / (ms_per_step / 1e3)},
+        "assemble_" + other: {"ms_per_step": other_ms, "value": routes / (other_ms / 1e3)},
+    }
+    # one process over all devices (the controller's own process, TopologyDB(
+    # devices=[...])): rank 0 alone, the others wait at the barrier
+    devices = [local] * world if os.environ.get("BENCH_DEVICE") else list(range(world))
+    sp = None
+    if rank == 0:
+        try:
+            mctx = _native.Context(devices)
+            mctx.upload(csr)
+            S = len(srcs)
+            ts = torch.from_numpy(np.ascontiguousarray(srcs, np.int32)).to(dev)
+            tab = torch.empty((S, csr.V), dtype=torch.int32, device=dev)
+            tab2 = None if packed else torch.empty_like(tab)
+            dist16 = torch.empty((S, csr.V), dtype=torch.int16, device=dev) \
+                if args.mode == "shortest" else None
+
+            def one():
+                if dist16 is not None:
+                    mctx.shortest_tables_device(ts.data_ptr(), S, dist16.data_ptr(),
+                                                tab.data_ptr(), tab2.data_ptr())
+                elif slots:
+                    mctx.dfs_tables_slots_device(ts.data_ptr(), S, tab.data_ptr())
+                elif packed:
+                    mctx.dfs_tables_packed_device(ts.data_ptr(), S, tab.data_ptr())
+                else:
+                    mctx.dfs_tables_device(ts.data_ptr(), S, tab.data_ptr(), tab2.data_ptr())
+            one()
+            mctx.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                one()
+            mctx.synchronize()
+            ms = (time.perf_counter() - t0) / reps * 1e3
+            sp = {"ms_per_step": ms, "value": routes / (ms / 1e3), "devices": devices,
+                  "kernel": mctx.last_kernel()}
+            mctx.close()
+        except Exception as e:   # noqa: BLE001 -- reported, not fatal for the headline
+            sp = {"error": repr(e)[:200], "devices": devices}
+    dist.barrier()
+    if sp is not None:
+        res["single_process"] = sp
+    return res
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -557,6 +661,7 @@ def main():
                 for b in bufs]
     pending = [[] for _ in range(nbuf)]
     counter = [0]
+    assemble = [args.assemble]
 
     def step(ev=None):
         k = counter[0] % nbuf
@@ -578,9 +683,10 @@ def main():
                                        tb[2].data_ptr())
         if ev is not None:
             ev[1].record(stream)
-        if world > 1:                       # assemble [sources][V] on every rank
+        if world > 1:                       # assemble [sources][V] on every rank / rank 0
             for t, g in zip(tb, gathered[k]):
-                pending[k].append(D.all_gather_rows_async(t, g))
+                pending[k].append(D.all_gather_rows_async(t, g) if assemble[0] == "all"
+                                  else D.gather_rows_to_root(t, g))
 
     def drain():
         for k in range(nbuf):
@@ -617,6 +723,11 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     routes = float(counts.sum()) * float(H)      # every host pair of these sources
     value = routes / (ms_per_step / 1e3)
+    multi = None
+    if world > 1:
+        multi = multi_gpu_extras(args, world, rank, local, dev, csr, srcs, per, packed, slots,
+                                 kern_ms, ms_per_step, routes, step, drain, bufs, gathered,
+                                 assemble)
     bytes_launch = algorithmic_bytes_per_source(V, E, args.mode, packed) * (hi - lo)
     achieved = bytes_launch / (kern_ms / 1e3) / 1e9
     per_entry = (4 if packed else 8) if args.mode == "dfs" else 10
@@ -668,6 +779,9 @@ def main():
         "switch_pair_routes_per_s": float(S) * V / (ms_per_step / 1e3),
         "teps": float(hi - lo) * E / (kern_ms / 1e3),
     }
+    if multi is not None:
+        out["multi_gpu"] = multi
+        out["config"]["assemble"] = args.assemble
     if rank == 0 and world == 1 and args.mode == "dfs" and \
             float(S) * V * (4 if packed else 8) <= 4e9:
         # the drop-in's host-buffer boundary: sources in, tables out over PCIe

@@ -1472,8 +1472,8 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int swz(int x) { return lds_swz(x); }   // common.h
 
-template <int NW, bool HOPS, bool PACKED>
-__global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
+template <int NW, bool HOPS, bool PACKED, bool C16>
+__global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
     int V, const uint16_t *__restrict__ adj, const uint16_t *__restrict__ radj,
     const uint32_t *__restrict__ deg, const int32_t *__restrict__ row_ptr,
     const int32_t *__restrict__ port, int W, const int32_t *__restrict__ ell_port,
@@ -1493,14 +1493,29 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int VW = (V + 1 + 31) >> 5;
     const int VWp = (VW + 3) & ~3;
-    const int CWp = (V + 1 + 255) & ~255;        // swizzled: whole 256-blocks
+    // C16 (compact): u16 counts in pairs, u16 parents + u8 slots -- 2,064
+    // dragonfly sources fit 9 per CU (all resident) instead of 6
+    const int CWp = C16 ? ((((V + 2) >> 1)) + 255) & ~255     // swizzled: whole 256-blocks
+                        : (V + 1 + 255) & ~255;
     const int SWp = (((V + 1) >> 1) + 3) & ~3;
-    const int PWp = (V + 255) & ~255;
+    const int PW = (V + 255) & ~255;                         // parent entries
+    const int PWp = C16 ? PW / 2 + PW / 4 : PW;
     uint32_t *vis = lds;
-    uint32_t *cnt = vis + VWp;                   // cnt[swz(v)]
+    uint32_t *cnt = vis + VWp;                   // cnt[swz(v)] (C16: swz(v >> 1), halves)
     uint16_t *stk = reinterpret_cast<uint16_t *>(cnt + CWp);
-    uint32_t *ps = cnt + CWp + SWp;              // ps[swz(v)]
+    uint32_t *ps = cnt + CWp + SWp;              // ps[swz(v)] = parent | slot << 16
+    uint16_t *ps16 = reinterpret_cast<uint16_t *>(ps);        // C16: ps16[swz(v)] = parent
+    uint8_t *sl8 = reinterpret_cast<uint8_t *>(ps16 + PW);    //      sl8[swz(v)] = slot
     uint16_t *dep = reinterpret_cast<uint16_t *>(ps + PWp);   // dep[v]
+    auto cnt_of = [&](int v) -> uint32_t {
+        if constexpr (C16) {
+            const uint32_t x = __hip_atomic_load(&cnt[swz(v >> 1)], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+            return (x >> ((v & 1) << 4)) & 0xFFFFu;
+        } else {
+            return __hip_atomic_load(&cnt[swz(v)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    };
     uint16_t *ring = reinterpret_cast<uint16_t *>(ps + PWp + (HOPS ? ((V + 1) >> 1) : 0));
     int *ctl = reinterpret_cast<int *>(ring + RING);   // [0] published [1] done [2+k] consumed
     const int lane = lane_id();
@@ -1530,17 +1545,34 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
         for (int i = threadIdx.x; i < VW; i += blockDim.x) vis[i] = 0u;
         // counts start at the out-degrees: U independent loads per thread in
         // flight before the LDS stores
-        for (int i0 = threadIdx.x; i0 <= V; i0 += U * blockDim.x) {
-            uint32_t dg[U];
+        if constexpr (C16) {                     // deg is padded to an even length
+            const int nw = (V + 2) >> 1;
+            for (int i0 = threadIdx.x; i0 < nw; i0 += U * blockDim.x) {
+                uint2 dg[U];
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const int i = i0 + k * (int)blockDim.x;
-                dg[k] = deg[i <= V ? i : V];
+                for (int k = 0; k < U; ++k) {
+                    const int i = i0 + k * (int)blockDim.x;
+                    dg[k] = reinterpret_cast<const uint2 *>(deg)[i < nw ? i : 0];
+                }
+#pragma unroll
+                for (int k = 0; k < U; ++k) {
+                    const int i = i0 + k * (int)blockDim.x;
+                    if (i < nw) cnt[swz(i)] = dg[k].x | (dg[k].y << 16);
+                }
             }
+        } else {
+            for (int i0 = threadIdx.x; i0 <= V; i0 += U * blockDim.x) {
+                uint32_t dg[U];
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
-                const int i = i0 + k * (int)blockDim.x;
-                if (i <= V) cnt[swz(i)] = dg[k];
+                for (int k = 0; k < U; ++k) {
+                    const int i = i0 + k * (int)blockDim.x;
+                    dg[k] = deg[i <= V ? i : V];
+                }
+#pragma unroll
+                for (int k = 0; k < U; ++k) {
+                    const int i = i0 + k * (int)blockDim.x;
+                    if (i <= V) cnt[swz(i)] = dg[k];
+                }
             }
         }
         if (threadIdx.x < 2 + S) ctl[threadIdx.x] = 0;
@@ -1555,7 +1587,8 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
             if (lane == 0) {
                 vis[s >> 5] |= 1u << (s & 31);
                 vis[V >> 5] |= 1u << (V & 31);
-                ps[swz(s)] = (uint32_t)s;
+                if (C16) ps16[swz(s)] = (uint16_t)s;
+                else ps[swz(s)] = (uint32_t)s;
                 if (HOPS) dep[s] = 0;
                 stk[0] = (uint16_t)s;
                 ring[0] = (uint16_t)s;           // s's in-neighbours lose one
@@ -1594,8 +1627,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                         const int at = sp - 1 - lane;
                         e = stk[at < 0 ? 0 : at];
                         e = lane < kk ? e : V;
-                        const uint32_t c = __hip_atomic_load(&cnt[swz(e)], __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+                        const uint32_t c = cnt_of(e);
                         m = __ballot(c != 0u);
                         if (m) break;
                         sp -= kk;
@@ -1682,15 +1714,19 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                 uint32_t cc = 0u;
                 if (fresh) {
                     atomicOr(&vis[x >> 5], 1u << (x & 31));
-                    ps[swz(x)] = (uint32_t)u | ((uint32_t)lane << 16);
+                    if (C16) {
+                        ps16[swz(x)] = (uint16_t)u;
+                        sl8[swz(x)] = (uint8_t)lane;
+                    } else {
+                        ps[swz(x)] = (uint32_t)u | ((uint32_t)lane << 16);
+                    }
                     if (HOPS) dep[x] = (uint16_t)(du + 1);
                     stk[sp + rank] = (uint16_t)x;
                     ring[(pub + rank) & (RING - 1)] = (uint16_t)x;
                     // children-first: the new stack top is these children
                     // (highest id on top); their counts are read while the
                     // prefetched rows are still in flight
-                    cc = __hip_atomic_load(&cnt[swz(x)], __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                    cc = cnt_of(x);
                 }
                 const uint64_t mc = __ballot(cc != 0u);
                 pub += c;
@@ -1750,11 +1786,15 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                 const int mine = lane < n ? (int)ring[(j + lane * S) & (RING - 1)] : V;
                 int r[G];
 #pragma unroll
-                for (int g = 0; g < G; ++g)
-                    r[g] = g < n ? (int)radj[(size_t)read_lane(mine, g) * 64 + lane] : V;
+                // unconditional: a slot past n loads the sentinel row V (L2
+                // resident); guarding each load measured 20 % slower
+                for (int g = 0; g < G; ++g) r[g] = radj[(size_t)read_lane(mine, g) * 64 + lane];
 #pragma unroll
                 for (int g = 0; g < G; ++g)
-                    if (g < n && r[g] != V) atomicSub(&cnt[swz(r[g])], 1u);
+                    if (g < n && r[g] != V) {
+                        if (C16) atomicSub(&cnt[swz(r[g] >> 1)], 1u << ((r[g] & 1) << 4));
+                        else atomicSub(&cnt[swz(r[g])], 1u);
+                    }
                 j += n * S;
                 if (lane == 0) __hip_atomic_store(&ctl[2 + w - 1], j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
@@ -1774,9 +1814,14 @@ __global__ __launch_bounds__(NW * 64) void dfs_async_kernel(
                 p[k] = -1;
                 sl[k] = -1;
                 if (v < V && ((vis[v >> 5] >> (v & 31)) & 1u)) {
-                    const uint32_t xx = ps[swz(v)];
-                    p[k] = (int)(xx & 0xFFFFu);
-                    if (v != s) sl[k] = (int)(xx >> 16);
+                    if (C16) {
+                        p[k] = (int)ps16[swz(v)];
+                        if (v != s) sl[k] = (int)sl8[swz(v)];
+                    } else {
+                        const uint32_t xx = ps[swz(v)];
+                        p[k] = (int)(xx & 0xFFFFu);
+                        if (v != s) sl[k] = (int)(xx >> 16);
+                    }
                 }
             }
 #pragma unroll
@@ -1969,12 +2014,13 @@ static size_t dfs_lds_bytes_count(int V, bool hops)
     return align16(4 * (VWp + CWp + SWp) + 4 * (size_t)V + (hops ? 2 * (size_t)V : 0));
 }
 
-static size_t dfs_lds_bytes_async(int V, bool hops)
+static size_t dfs_lds_bytes_async(int V, bool hops, bool c16 = false)
 {
     const size_t VWp = (size_t)((((V + 1 + 31) >> 5) + 3) & ~3);
-    const size_t CWp = (size_t)((V + 1 + 255) & ~255);
+    const size_t CWp = c16 ? (size_t)((((V + 2) >> 1) + 255) & ~255) : (size_t)((V + 1 + 255) & ~255);
     const size_t SWp = (size_t)((((V + 1) >> 1) + 3) & ~3);
-    const size_t PWp = (size_t)((V + 255) & ~255);
+    const size_t PW = (size_t)((V + 255) & ~255);
+    const size_t PWp = c16 ? PW / 2 + PW / 4 : PW;
     return align16(4 * (VWp + CWp + SWp) + 4 * PWp +
                    (hops ? 4 * (size_t)((V + 1) >> 1) : 0) + 2 * 512 + 4 * 16);
 }
@@ -2312,13 +2358,23 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
     const bool coop = !count && coop_ok && (force ? !strcmp(force, "coop") : small);
     if (async) {
         int *err = ctx->d_err;
-        const size_t cl = dfs_lds_bytes_async(V, hops);
-        size_t cpc = SDNR_LDS_PER_CU / cl;
-        if (cpc > 8) cpc = 8;
-        if (cpc < 1) cpc = 1;
+        const int nw = dfs_async_waves(ctx);
+        // workgroups per CU: LDS, and the 32 wave slots; the compact layout
+        // (u16 counts, u16 parents + u8 slots) where it holds more sources
+        // at once and the full layout cannot hold them all (dragonfly 2,064
+        // sources: 9 x 3 waves per CU vs 6); SDNROUTE_DFS_C16=0|1 forces it
+        auto per_cu = [&](bool c) {
+            size_t b = SDNR_LDS_PER_CU / dfs_lds_bytes_async(V, hops, c);
+            if (b > (size_t)(32 / nw)) b = 32 / nw;
+            return b < 1 ? (size_t)1 : b;
+        };
+        bool c16 = per_cu(true) > per_cu(false) &&
+                   (size_t)ctx->num_cus * per_cu(false) < (size_t)nsrc;
+        if (const char *f = getenv("SDNROUTE_DFS_C16")) c16 = !strcmp(f, "1");
+        const size_t cl = dfs_lds_bytes_async(V, hops, c16);
+        const size_t cpc = per_cu(c16);
         int cgrid = (int)((size_t)ctx->num_cus * cpc);
         if (cgrid > nsrc) cgrid = nsrc;
-        const int nw = dfs_async_waves(ctx);
         // the search wave issues at raised priority over the decrement
         // workers (dragonfly 0.316 -> 0.300 ms, k=48 unchanged)
         static const char *names[] = {"", "", "dfs_async_kernel<2>", "dfs_async_kernel<3>",
@@ -2327,7 +2383,7 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         ctx->last_kernel = names[nw];
 #define SDNR_ASYNC_P(N_, H_, P_)                                                             \
     do {                                                                                     \
-        auto k = dfs_async_kernel<N_, H_, P_>;                                               \
+        auto k = c16 ? dfs_async_kernel<N_, H_, P_, true> : dfs_async_kernel<N_, H_, P_, false>; \
         allow_full_lds(k);                                                                   \
         hipLaunchKernelGGL(k, dim3(cgrid), dim3(N_ * 64), cl, ctx->stream, V, ctx->adj16,    \
                            ctx->radj16, ctx->deg32, ctx->row_ptr, ctx->port, ctx->W,         \

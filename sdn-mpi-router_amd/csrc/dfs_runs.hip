@@ -441,7 +441,7 @@ __global__ __launch_bounds__(1024) void dfs_runs_kernel(
                     int r[kRunsG];
 #pragma unroll
                     for (int g = 0; g < kRunsG; ++g)
-                        r[g] = g < n ? (int)radj[(size_t)read_lane(mine, g) * 64 + lane] : V;
+                        r[g] = radj[(size_t)read_lane(mine, g) * 64 + lane];   // past n: row V
 #pragma unroll
                     for (int g = 0; g < kRunsG; ++g)
                         if (g < n && r[g] != V) cnt_dec(cntw, r[g]);

@@ -15,7 +15,7 @@ import torch
 import torch.distributed as dist
 
 __all__ = ["shard_bounds", "padded_shard", "all_gather_rows", "all_gather_rows_async", "unpad",
-           "sharded_route_tables"]
+           "sharded_route_tables", "gather_rows_to_root"]
 
 
 def shard_bounds(n, world, rank):
@@ -85,6 +85,49 @@ def all_gather_rows_async(local, out, group=None):
 class _Done(object):
     def wait(self):
         return True
+
+
+class _Works(object):
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        return True
+
+
+def gather_rows_to_root(local, out, group=None, root=0):
+    """Rows [per, V] of every rank into ``out`` [world*per, V] on ``root`` only
+    (rank order; ``out`` is ignored elsewhere): the tables assembled on the
+    controller's GPU, SURVEY.md 8(e)'s "or on GPU 0 only" -- world-1 point-to-
+    point transfers into the root instead of a ring all-gather to everyone.
+    Returns a handle to ``wait()`` on."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    src = local.contiguous()
+    if src.dtype == torch.int16:             # no 16-bit integers in the collectives: bytes
+        src = src.view(torch.uint8)
+        out = out.view(torch.uint8) if out is not None else None
+    per = src.shape[0]
+    groot = dist.get_global_rank(group, root) if group is not None else root
+    if dist.get_backend(group) == "nccl":
+        if rank == root:
+            out[root * per:(root + 1) * per].copy_(src)
+            ops = [dist.P2POp(dist.irecv, out[r * per:(r + 1) * per],
+                              dist.get_global_rank(group, r) if group is not None else r,
+                              group=group)
+                   for r in range(world) if r != root]
+        else:
+            ops = [dist.P2POp(dist.isend, src, groot, group=group)]
+        return _Works(dist.batch_isend_irecv(ops)) if ops else _Done()
+    # gloo (CPU, rehearsal): through host memory
+    host = src.cpu()
+    parts = [torch.empty_like(host) for _ in range(world)] if rank == root else None
+    dist.gather(host, parts, dst=groot, group=group)
+    if rank == root:
+        out.copy_(torch.cat(parts).to(out.device))
+    return _Done()
 
 
 def unpad(table, n):

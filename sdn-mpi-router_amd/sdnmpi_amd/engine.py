@@ -18,8 +18,8 @@ far, within a byte budget, in a fixed-capacity pool of compact rows:
   bytes per entry; the next hop's port is looked up in the CSR on demand.
 
 Slots are taken from a free list and given back on eviction or when a graph
-change invalidates the row; no operation copies the pool (it grows by
-doubling up to the budget), free slots hold all-unreached rows.  A single
+change invalidates the row; the pool is allocated once (min(budget rows, V)
+rows) and no operation copies it, free slots hold all-unreached rows.  A single
 ``find_route`` copies back one table row (V entries, kept in a small host
 cache), a batch is expanded on the device.  Expansion follows the
 reference's ``_route_to_fdb`` (:127-138): one ``(dpid, out_port)`` per switch
@@ -391,9 +391,9 @@ class _Pool(object):
     vertices oldest first.  Adding takes slots from the free list (evicting
     the oldest unprotected rows when the budget is full), dropping gives
     them back and refills them with the ``blank`` row (all unreached), so a
-    test over the whole store never sees garbage.  The store grows by
-    doubling up to ``cap`` rows; it is never concatenated, re-indexed or
-    copied otherwise."""
+    test over the whole store never sees garbage.  The store is allocated
+    once, min(cap, V) rows, on first use; it is never grown, concatenated,
+    re-indexed or copied."""
 
     def __init__(self, budget, row_bytes, blanks):
         self.budget = budget
@@ -428,10 +428,13 @@ class _Pool(object):
         return s
 
     def _grow(self, need, like):
-        """Make at least ``need`` slots exist (doubling, at most cap)."""
+        """Make at least ``need`` slots exist.  The first call allocates the
+        whole store -- min(cap, V) rows: a graph has at most V distinct rows
+        -- so it never grows again (and never holds more than the budget)."""
         if need <= self.size:
             return
-        new = min(self.cap(), max(need, 2 * self.size, 16))
+        V = int(like[0].shape[1]) if like[0].ndim > 1 else 1
+        new = max(need, min(self.cap(), V))
         fresh = []
         for a, b in zip(like, self.blanks):
             shape = (new,) + tuple(a.shape[1:])

@@ -216,10 +216,37 @@ def test_dfs_runs_fullsize(ctx, monkeypatch, name, slots):
     _check_pairs(g, fabric, p, t, srcs)
 
 
+@pytest.mark.parametrize("c16", ["0", "1"])
+@pytest.mark.parametrize("layout", ["int32", "hops"])
+@pytest.mark.parametrize("name", G.SMALL)
+def test_dfs_async_compact_lds(ctx, monkeypatch, name, layout, c16):
+    """dfs_async_kernel with the compact LDS layout (u16 counts in pairs, u16
+    parents + u8 slots; the dragonfly default) and without, every source."""
+    _strategy(monkeypatch, "async")
+    monkeypatch.setenv("SDNROUTE_DFS_C16", c16)
+    csr = G.Golden(name).fabric().csr()
+    srcs = np.arange(csr.V, dtype=np.int32)
+    _check_dfs(ctx, csr, srcs, hops=layout == "hops")
+
+
+def test_dfs_dragonfly_one_residency_round(ctx):
+    """Dragonfly a16 h8: all 2,064 sources at once with the compact layout
+    (the default there), bit-exact packed trees."""
+    fabric = T.dragonfly(16, 8, 8)
+    csr = fabric.csr()
+    srcs = np.arange(csr.V, dtype=np.int32)
+    ctx.upload(csr)
+    tree = ctx.dfs_tables_packed(srcs)
+    po, to, _ = O.dfs_tables(csr, srcs, with_hops=False, nthreads=NTHREADS)
+    np.testing.assert_array_equal(tree, _pack(po, to))
+
+
+@pytest.mark.parametrize("c16", ["0", "1"])
 @pytest.mark.parametrize("waves", [2, 3, 4, 5, 6])
 @pytest.mark.parametrize("name", ["fat_tree_k8", "jellyfish_n60_r5", "torus_5x3x2"])
-def test_dfs_packed_async_waves(ctx, monkeypatch, name, waves):
+def test_dfs_packed_async_waves(ctx, monkeypatch, name, waves, c16):
     _strategy(monkeypatch, "async")
+    monkeypatch.setenv("SDNROUTE_DFS_C16", c16)
     monkeypatch.setenv("SDNROUTE_DFS_ASYNC_WAVES", str(waves))
     csr = G.Golden(name).fabric().csr()
     srcs = np.arange(csr.V, dtype=np.int32)
