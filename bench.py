@@ -89,6 +89,17 @@ def _traffic(key):
         return None
 
 
+def _measured(traffic, kern_ms):
+    """Measured HBM side of a roofline: the PMC traffic per launch
+    (profiles/traffic.json, FETCH_SIZE / WRITE_SIZE with the factors
+    tools/calib_traffic.py measured) over the live kernel time, and its
+    fraction of the HBM peak -- beside the algorithmic frac."""
+    if not traffic or not kern_ms:
+        return {"hbm_gbs": None, "hbm_frac": None}
+    gbs = traffic / (kern_ms / 1e3) / 1e9
+    return {"hbm_gbs": gbs, "hbm_frac": gbs / HBM_PEAK_GBS}
+
+
 def algorithmic_bytes_per_source(V, E, mode, packed=False):
     if mode == "dfs":
         # row_ptr + col (CSR read per source) + tree-edge port reads + table writes
@@ -352,7 +363,7 @@ def main_flows(args, world, rank, local, dev):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": ctx.last_kernel(), "kernel_ms": kern_ms,
-                     "bytes_per_launch": bytes_launch},
+                     "bytes_per_launch": bytes_launch, **_measured(traffic, kern_ms)},
         "entries_per_s": float(total) * world / (ms / 1e3),
     }
     if rank == 0:
@@ -421,7 +432,8 @@ def main_ecmp(args, world, rank, local, dev):
                      "frac": achieved / HBM_PEAK_GBS, "traffic": _traffic("%s/ecmp/N%d" % (
                          args.fabric, world)),
                      "kernel": ctx.last_kernel(), "kernel_ms": kern_ms,
-                     "bytes_per_launch": bytes_launch},
+                     "bytes_per_launch": bytes_launch,
+                     **_measured(_traffic("%s/ecmp/N%d" % (args.fabric, world)), kern_ms)},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -478,7 +490,8 @@ def main_apsp(args, world, rank, local, dev):
                      "frac": achieved / peak, "traffic": _traffic("%s/apsp/N1" % args.fabric),
                      "kernel": ctx.last_kernel(),
                      "kernel_ms": kern_ms, "ops_per_launch": ops, "passes": passes,
-                     "padded_ops_per_launch": passes * 2.0 * float(Vp) ** 3},
+                     "padded_ops_per_launch": passes * 2.0 * float(Vp) ** 3,
+                     **_measured(_traffic("%s/apsp/N1" % args.fabric), kern_ms)},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -775,6 +788,7 @@ def main():
             # port) read once + this launch's tables written once
             "compulsory_bytes": compulsory,
             "compulsory_gbs": compulsory / (kern_ms / 1e3) / 1e9,
+            **_measured(traffic, kern_ms),
         },
         "switch_pair_routes_per_s": float(S) * V / (ms_per_step / 1e3),
         "teps": float(hi - lo) * E / (kern_ms / 1e3),

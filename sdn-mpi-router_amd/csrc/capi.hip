@@ -94,6 +94,10 @@ static void free_graph(sdnr_ctx *c)
     c->runs_R = 0;
     if (c->adj16) (void)hipFree(c->adj16);
     if (c->deg32) (void)hipFree(c->deg32);
+    if (c->radjw) (void)hipFree(c->radjw);
+    c->radjw = nullptr;
+    if (c->radjc) (void)hipFree(c->radjc);
+    c->radjc = nullptr;
     if (c->ell16) (void)hipFree(c->ell16);
     if (c->ell_hi) (void)hipFree(c->ell_hi);
     c->ell16 = nullptr;
@@ -456,6 +460,43 @@ static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *
                 if (he == hipSuccess)
                     he = hipMemcpyAsync(ctx->radj16, r16.data(), rows * 2, hipMemcpyHostToDevice,
                                         ctx->stream);
+            }
+        }
+        // in-rows as the async DFS workers' count indices: lds_swz(x); the
+        // padding of slot l a dummy word of its own past the counts (one
+        // shared dummy made every ds_sub a 16-way same-address conflict:
+        // 3x slower) (dfs.hip, kFlagPreSwz)
+        // (dummies right past the swizzled counts, inside the 256-word
+        // padding where it has room: a +256-B LDS block per workgroup took
+        // k=48 from 5 to 4 workgroups per CU)
+        const size_t dummy = (((size_t)V + 1 + 31) & ~(size_t)31);
+        if (he == hipSuccess && maxin <= SDNR_WAVE && dummy + SDNR_WAVE <= 0xFFFF) {
+            std::vector<uint16_t> w16(r16.size());
+            const std::vector<uint16_t> &src16 = sym ? a16 : r16;
+            for (size_t i = 0; i < w16.size(); ++i) {
+                const int x = src16[i];
+                w16[i] = (uint16_t)(x == V ? (int)(dummy + i % SDNR_WAVE) : (x ^ ((x >> 3) & 31)));
+            }
+            he = hipMalloc(reinterpret_cast<void **>(&ctx->radjw), w16.size() * 2);
+            if (he == hipSuccess)
+                he = hipMemcpyAsync(ctx->radjw, w16.data(), w16.size() * 2, hipMemcpyHostToDevice,
+                                    ctx->stream);
+            if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
+            // the same for the compact-LDS kernel (u16 counts in pairs):
+            // entry = lds_swz(x >> 1) << 1 | (x & 1), dummies dummyc + lane
+            const size_t dummyc = ((((size_t)V + 2) >> 1) + 31) & ~(size_t)31;
+            if (he == hipSuccess && 2 * (dummyc + SDNR_WAVE) <= 0xFFFF) {
+                for (size_t i = 0; i < w16.size(); ++i) {
+                    const int x = src16[i];
+                    const int h = x >> 1;
+                    w16[i] = (uint16_t)(x == V ? (int)(2 * (dummyc + i % SDNR_WAVE))
+                                               : ((h ^ ((h >> 3) & 31)) << 1) | (x & 1));
+                }
+                he = hipMalloc(reinterpret_cast<void **>(&ctx->radjc), w16.size() * 2);
+                if (he == hipSuccess)
+                    he = hipMemcpyAsync(ctx->radjc, w16.data(), w16.size() * 2,
+                                        hipMemcpyHostToDevice, ctx->stream);
+                if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
             }
         }
         // the out-rows as arithmetic runs for the LDS-row DFS (dfs_runs.hip)

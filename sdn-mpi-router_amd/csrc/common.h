@@ -58,6 +58,8 @@ struct sdnr_ctx {
     uint16_t *adj16 = nullptr;          // (V+1) rows x 64 u16, sentinel V (V < 65535)
     uint16_t *radj16 = nullptr;         // in-neighbour rows, same layout (== adj16 if symmetric)
     uint32_t *deg32 = nullptr;          // out-degrees of 0..V (sentinel V: 0)
+    uint16_t *radjw = nullptr;          // radj16 as swizzled count indices (async DFS workers)
+    uint16_t *radjc = nullptr;          // ... for the compact-LDS form (word << 1 | half)
     bool radj_owned = false;
     // out-rows as arithmetic runs (dfs_runs.hip): (V+1) rows x runs_R words
     // of start | stride << 16 | count << 25

@@ -1058,6 +1058,8 @@ constexpr int kSplitQ = 64;                    // queued records per search wave
 // slot instead of the port
 // (diagnostic) no port lookups in the writer
 constexpr int kFlagPrio = 1, kFlagNT = 2, kFlagNoStore = 4, kFlagNoPort = 8;
+// dfs_async_kernel: the worker rows are pre-swizzled count indices (radjw)
+constexpr int kFlagPreSwz = 16;
 
 template <int FMT>
 __device__ __forceinline__ int split_row(const void *__restrict__ rows,
@@ -1495,8 +1497,9 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
     const int VWp = (VW + 3) & ~3;
     // C16 (compact): u16 counts in pairs, u16 parents + u8 slots -- 2,064
     // dragonfly sources fit 9 per CU (all resident) instead of 6
-    const int CWp = C16 ? ((((V + 2) >> 1)) + 255) & ~255     // swizzled: whole 256-blocks
-                        : (V + 1 + 255) & ~255;
+    // count words, swizzled within 32-word groups, then 64 dummy words (the
+    // pre-swizzled in-rows' padding targets, one per lane), whole 256-blocks
+    const int CWp = ((((C16 ? (V + 2) >> 1 : V + 1) + 31) & ~31) + 64 + 255) & ~255;
     const int SWp = (((V + 1) >> 1) + 3) & ~3;
     const int PW = (V + 255) & ~255;                         // parent entries
     const int PWp = C16 ? PW / 2 + PW / 4 : PW;
@@ -1785,16 +1788,29 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                 const int n = (P - j + S - 1) / S < G ? (P - j + S - 1) / S : G;
                 const int mine = lane < n ? (int)ring[(j + lane * S) & (RING - 1)] : V;
                 int r[G];
-#pragma unroll
                 // unconditional: a slot past n loads the sentinel row V (L2
                 // resident); guarding each load measured 20 % slower
-                for (int g = 0; g < G; ++g) r[g] = radj[(size_t)read_lane(mine, g) * 64 + lane];
 #pragma unroll
-                for (int g = 0; g < G; ++g)
-                    if (g < n && r[g] != V) {
-                        if (C16) atomicSub(&cnt[swz(r[g] >> 1)], 1u << ((r[g] & 1) << 4));
-                        else atomicSub(&cnt[swz(r[g])], 1u);
-                    }
+                for (int g = 0; g < G; ++g) r[g] = radj[(size_t)read_lane(mine, g) * 64 + lane];
+                if (flags & kFlagPreSwz) {
+                    // pre-swizzled in-rows: entries are count-word indices
+                    // (C16: word << 1 | half), padding points at a dummy
+                    // word of its lane past the counts -- no compare, mask
+                    // or swizzle arithmetic per child
+#pragma unroll
+                    for (int g = 0; g < G; ++g)
+                        if (g < n) {
+                            if (C16) atomicSub(&cnt[r[g] >> 1], 1u << ((r[g] & 1) << 4));
+                            else atomicSub(&cnt[r[g]], 1u);
+                        }
+                } else {
+#pragma unroll
+                    for (int g = 0; g < G; ++g)
+                        if (g < n && r[g] != V) {
+                            if (C16) atomicSub(&cnt[swz(r[g] >> 1)], 1u << ((r[g] & 1) << 4));
+                            else atomicSub(&cnt[swz(r[g])], 1u);
+                        }
+                }
                 j += n * S;
                 if (lane == 0) __hip_atomic_store(&ctl[2 + w - 1], j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
@@ -2017,7 +2033,7 @@ static size_t dfs_lds_bytes_count(int V, bool hops)
 static size_t dfs_lds_bytes_async(int V, bool hops, bool c16 = false)
 {
     const size_t VWp = (size_t)((((V + 1 + 31) >> 5) + 3) & ~3);
-    const size_t CWp = c16 ? (size_t)((((V + 2) >> 1) + 255) & ~255) : (size_t)((V + 1 + 255) & ~255);
+    const size_t CWp = (size_t)(((((c16 ? (V + 2) >> 1 : V + 1) + 31) & ~31) + 64 + 255) & ~255);
     const size_t SWp = (size_t)((((V + 1) >> 1) + 3) & ~3);
     const size_t PW = (size_t)((V + 255) & ~255);
     const size_t PWp = c16 ? PW / 2 + PW / 4 : PW;
@@ -2373,6 +2389,11 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         if (const char *f = getenv("SDNROUTE_DFS_C16")) c16 = !strcmp(f, "1");
         const size_t cl = dfs_lds_bytes_async(V, hops, c16);
         const size_t cpc = per_cu(c16);
+        // pre-swizzled worker rows (SDNROUTE_DFS_PRESWZ=0 keeps the plain ones)
+        const char *pz = getenv("SDNROUTE_DFS_PRESWZ");
+        const uint16_t *rw = c16 ? ctx->radjc : ctx->radjw;
+        const bool preswz = rw && !(pz && !strcmp(pz, "0"));
+        const int aflags = dfs_flags(kFlagPrio) | (preswz ? kFlagPreSwz : 0);
         int cgrid = (int)((size_t)ctx->num_cus * cpc);
         if (cgrid > nsrc) cgrid = nsrc;
         // the search wave issues at raised priority over the decrement
@@ -2386,10 +2407,10 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         auto k = c16 ? dfs_async_kernel<N_, H_, P_, true> : dfs_async_kernel<N_, H_, P_, false>; \
         allow_full_lds(k);                                                                   \
         hipLaunchKernelGGL(k, dim3(cgrid), dim3(N_ * 64), cl, ctx->stream, V, ctx->adj16,    \
-                           ctx->radj16, ctx->deg32, ctx->row_ptr, ctx->port, ctx->W,         \
-                           ctx->ell_port, d_src, nsrc,                                       \
+                           preswz ? rw : ctx->radj16, ctx->deg32, ctx->row_ptr,              \
+                           ctx->port, ctx->W, ctx->ell_port, d_src, nsrc,                    \
                            P_ ? reinterpret_cast<int32_t *>(d_tree) : d_parent, d_port,      \
-                           d_hops, err, dfs_flags(kFlagPrio));                               \
+                           d_hops, err, aflags);                                             \
     } while (0)
 #define SDNR_ASYNC(N_, H_) SDNR_ASYNC_P(N_, H_, false)
         if (packed) {

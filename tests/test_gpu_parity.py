@@ -216,14 +216,18 @@ def test_dfs_runs_fullsize(ctx, monkeypatch, name, slots):
     _check_pairs(g, fabric, p, t, srcs)
 
 
-@pytest.mark.parametrize("c16", ["0", "1"])
+@pytest.mark.parametrize("c16", ["0", "1", "0plain", "1plain"])
 @pytest.mark.parametrize("layout", ["int32", "hops"])
 @pytest.mark.parametrize("name", G.SMALL)
 def test_dfs_async_compact_lds(ctx, monkeypatch, name, layout, c16):
     """dfs_async_kernel with the compact LDS layout (u16 counts in pairs, u16
-    parents + u8 slots; the dragonfly default) and without, every source."""
+    parents + u8 slots; the dragonfly default) and without -- with the
+    workers' pre-swizzled in-rows (the default) or the plain ones -- every
+    source."""
     _strategy(monkeypatch, "async")
-    monkeypatch.setenv("SDNROUTE_DFS_C16", c16)
+    monkeypatch.setenv("SDNROUTE_DFS_C16", c16[0])
+    if c16.endswith("plain"):
+        monkeypatch.setenv("SDNROUTE_DFS_PRESWZ", "0")
     csr = G.Golden(name).fabric().csr()
     srcs = np.arange(csr.V, dtype=np.int32)
     _check_dfs(ctx, csr, srcs, hops=layout == "hops")

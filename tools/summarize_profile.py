@@ -5,9 +5,15 @@
 
 Writes <out>_kernel_stats.csv (rocprofv3 --kernel-trace --stats, verbatim),
 <out>_pmc.json (per-dispatch means of every PMC counter, per kernel) and
-<out>_summary.md (human-readable, with the HBM traffic derived as
-MI355X_MICROARCH.md prescribes: FETCH_SIZE x 2 on gfx950 for wide streaming
-reads, WRITE_SIZE as reported, both in KiB per dispatch).
+<out>_summary.md (human-readable, with the HBM traffic derived from
+FETCH_SIZE / WRITE_SIZE (KiB per dispatch) with the factors measured by the
+known-byte calibration of tools/calib_traffic.hip, profiles/
+r03_traffic_calibration.json: every read shape the route kernels use -- 16-B
+and 4-B coalesced reads, u16 128-B rows, 4-B random gathers -- is fetched as
+128-B requests that FETCH_SIZE tallies at 64 B (factor 2.0); WRITE_SIZE equals
+the bytes of the memory-side write requests for both coalesced stores (64-B
+requests) and scattered 4-B stores (32-B masked requests, 8x the useful bytes),
+factor 1.0).
 """
 import collections
 import csv
@@ -16,6 +22,38 @@ import json
 import os
 import shutil
 import sys
+
+
+CALIBRATION = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles",
+                           "r03_traffic_calibration.json")
+
+
+def factors(path=CALIBRATION):
+    """(fetch, write) multipliers from the calibration file: the median over
+    the read shapes of line bytes / FETCH_SIZE bytes, and over the write
+    shapes of request bytes / WRITE_SIZE bytes.  A shape whose counter
+    disagrees with its request count by more than 2x (a kernel the compiler
+    thinned) is left out."""
+    try:
+        cal = json.load(open(path))
+    except (OSError, ValueError):
+        return 2.0, 1.0     # MI355X_MICROARCH.md's gfx950 correction
+    def med(xs, default):
+        xs = sorted(xs)
+        return xs[len(xs) // 2] if xs else default
+    rd = [r["fetch_factor"] for r in cal.values() if r.get("kind") == "read" and
+          "fetch_factor" in r and r.get("read_req_bytes") and
+          0.5 < r["read_req_bytes"] / r["line_bytes"] < 2.0]
+    wr = [r["write_factor"] for r in cal.values() if r.get("kind") == "write" and "write_factor" in r]
+    return med(rd, 2.0), med(wr, 1.0)
+
+
+FETCH_FACTOR, WRITE_FACTOR = factors()
+
+
+def hbm_bytes(c):
+    """Corrected HBM bytes per dispatch from a counter dict (KiB values)."""
+    return (FETCH_FACTOR * c.get("FETCH_SIZE", 0.0) + WRITE_FACTOR * c.get("WRITE_SIZE", 0.0)) * 1024.0
 
 
 def main(src, out):
@@ -53,11 +91,9 @@ def main(src, out):
         for name in sorted(c):
             lines.append("- %s: %.4g per dispatch" % (name, c[name]))
         if "FETCH_SIZE" in c or "WRITE_SIZE" in c:
-            fetch = c.get("FETCH_SIZE", 0.0)
-            write = c.get("WRITE_SIZE", 0.0)
-            lines.append("- HBM traffic per dispatch (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 "
-                         "correction of MI355X_MICROARCH.md): %.1f MB"
-                         % ((2 * fetch + write) * 1024 / 1e6))
+            lines.append("- HBM traffic per dispatch (FETCH_SIZE x %.3g + WRITE_SIZE x %.3g, "
+                         "factors measured by tools/calib_traffic.hip): %.1f MB"
+                         % (FETCH_FACTOR, WRITE_FACTOR, hbm_bytes(c) / 1e6))
         if "SQ_WAVE_CYCLES" in c:
             wc = c["SQ_WAVE_CYCLES"]
             lines.append("- wave-cycle split: wait %.0f%%, issue-stall %.0f%%, active %.0f%%" % (
@@ -84,7 +120,7 @@ def record_traffic(pmc, key, kernel_prefix, path, steps=None):
         c = hits[0]["counters"]
         if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
             raise SystemExit("FETCH_SIZE / WRITE_SIZE missing for %r" % pre)
-        per = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+        per = hbm_bytes(c)
         tb += per * (hits[0]["dispatches"] / float(steps) if len(prefixes) > 1 else 1.0)
     data = json.load(open(path)) if os.path.exists(path) else {}
     data[key] = tb
