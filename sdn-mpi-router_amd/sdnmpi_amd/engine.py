@@ -40,12 +40,16 @@ from . import _native
 from .graph import empty_csr
 
 __all__ = ["RouteEngine", "TableCache", "tree_path", "expand_tree_paths",
-           "shortest_paths_lex", "DEFAULT_TABLE_BUDGET", "tree_layout", "dfs_row_bytes",
+           "shortest_paths_lex", "count_shortest_paths", "ECMP_LIMIT", "DEFAULT_TABLE_BUDGET", "tree_layout", "dfs_row_bytes",
            "sp_row_bytes"]
 
 # bytes of device tables one TableCache keeps per route mode before it
 # evicts rows (SDNROUTE_TABLE_BUDGET overrides); the torus 32^3 default-route
 # tables of every source take 6.4 GB in the pool, Jellyfish 100k's 80 GB
+# Largest ECMP set either find_route(..., multiple=True) path builds; above
+# it both raise MemoryError (the reference's enumeration runs out of memory
+# long before).
+ECMP_LIMIT = 1 << 40
 DEFAULT_TABLE_BUDGET = int(os.environ.get("SDNROUTE_TABLE_BUDGET", str(24 << 30)))
 HOST_ROW_CACHE = 256            # table rows kept on the host for find_route
 COMPUTE_ROWS = 4096             # rows per engine call when filling the pool
@@ -313,7 +317,7 @@ class RouteEngine(object):
         self.ctx.synchronize()
         flat = t.as_tensor(rows * V + srcs, dtype=t.int64, device=self.dev)
         cnt_u = paths.view(-1).index_select(0, flat).cpu().numpy().view(np.uint64)
-        if (cnt_u > np.uint64(1 << 40)).any():
+        if (cnt_u > np.uint64(ECMP_LIMIT)).any():
             raise MemoryError("ECMP set too large to enumerate")
         cnt = cnt_u.astype(np.int64)
         dsel = dist.view(-1).index_select(0, flat).cpu().numpy().view(np.uint16)
@@ -686,10 +690,44 @@ def tree_path(parent_row, s, d):
     return seq
 
 
+def count_shortest_paths(row_ptr, col, dist_row, s, d, limit=None):
+    """Number of shortest s->d routes: a DP over the part of the
+    shortest-path DAG reachable from s, deepest level first (the host twin of
+    ecmp.hip's per-row count).  Stops counting once ``limit`` is passed and
+    returns limit + 1."""
+    dist_row = np.asarray(dist_row)
+    want = int(dist_row[s])
+    levels = [[int(s)]]
+    seen = {int(s)}
+    for _ in range(want):             # BFS down the DAG, one level at a time
+        nxt = []
+        for x in levels[-1]:
+            dn = int(dist_row[x]) - 1
+            for e in range(int(row_ptr[x]), int(row_ptr[x + 1])):
+                n = int(col[e])
+                if int(dist_row[n]) == dn and n not in seen:
+                    seen.add(n)
+                    nxt.append(n)
+        levels.append(nxt)
+    cnt = {int(d): 1}
+    cap = None if limit is None else int(limit) + 1
+    for lv in reversed(levels[:-1]):
+        for x in lv:
+            dn, c = int(dist_row[x]) - 1, 0
+            for e in range(int(row_ptr[x]), int(row_ptr[x + 1])):
+                n = int(col[e])
+                if int(dist_row[n]) == dn:
+                    c += cnt.get(n, 0)
+            cnt[x] = c if cap is None else min(c, cap)
+    return cnt.get(int(s), 0)
+
+
 def shortest_paths_lex(row_ptr, col, dist_row, s, d):
     """Every shortest s->d vertex sequence in lexicographic dpid order (the
     order _find_routes_bfs returns them, topology_db.py:95-122): walk the
-    shortest-path DAG (dist_row = hops to d) taking successors ascending."""
+    shortest-path DAG (dist_row = hops to d) taking successors ascending.
+    Sets above ECMP_LIMIT routes raise MemoryError before any is built, as
+    the batched device path (RouteEngine.ecmp) does."""
     INF = _native.DIST_INF
     dist_row = np.asarray(dist_row)
     if dist_row.dtype == np.int16:
@@ -697,6 +735,8 @@ def shortest_paths_lex(row_ptr, col, dist_row, s, d):
     dist_row = np.where(dist_row < 0, INF, dist_row)
     if int(dist_row[s]) == INF:
         return []
+    if count_shortest_paths(row_ptr, col, dist_row, s, d, ECMP_LIMIT) > ECMP_LIMIT:
+        raise MemoryError("ECMP set too large to enumerate")
     out = []
     acc = [int(s)]
 

@@ -9,7 +9,8 @@ import pytest
 
 from oracle import oracle as O
 from sdnmpi_amd import topologies as T
-from sdnmpi_amd.engine import expand_tree_paths, shortest_paths_lex, tree_path
+from sdnmpi_amd.engine import (ECMP_LIMIT, count_shortest_paths, expand_tree_paths,
+                               shortest_paths_lex, tree_path)
 from sdnmpi_amd.graph import export_graph
 from sdnmpi_amd.util.topology_db import TopologyDB
 
@@ -119,6 +120,27 @@ def test_shortest_paths_lex_matches_reference_order():
             assert seqs == sorted(seqs)
             for q in seqs:
                 assert len(q) - 1 == dist[d, s] and len(set(q)) == len(q)
+
+
+def test_shortest_paths_count_and_limit():
+    # the host count equals the enumeration's length (fat-tree, small torus)
+    for fab in (T.fat_tree(4), T.torus3d(4, 4, 4)):
+        c = fab.csr()
+        dist, _, _ = O.dest_tables(c, np.arange(c.V, dtype=np.int32))
+        for s in range(0, c.V, 7):
+            for d in range(0, c.V, 5):
+                if dist[d, s] == 0xFFFF:
+                    continue
+                n = len(shortest_paths_lex(c.row_ptr, c.col, dist[d], s, d))
+                assert count_shortest_paths(c.row_ptr, c.col, dist[d], s, d) == n
+    # torus 32^3 antipodal pair: 48!/(16!)^3 ~ 1e21 routes -> MemoryError
+    # before enumerating, like the batched device path (RouteEngine.ecmp)
+    c = T.torus3d(32, 32, 32).csr()
+    dist, _, _ = O.dest_tables(c, np.array([0], np.int32))
+    far = 16 * 1024 + 16 * 32 + 16
+    assert count_shortest_paths(c.row_ptr, c.col, dist[0], far, 0, ECMP_LIMIT) > ECMP_LIMIT
+    with pytest.raises(MemoryError):
+        shortest_paths_lex(c.row_ptr, c.col, dist[0], far, 0)
 
 
 def test_unpack_tree_layout():
