@@ -1,0 +1,10 @@
+#!/bin/bash
+# round-3: plane-chunk placement probe; split-DFS stamps (torus, Jellyfish); NT / no-store flag sweeps
+OUT=gpurun_out/r3r; mkdir -p $OUT
+timeout -k 10 400 python tools/bimodal_chunk.py 8 64 56 48 40 32 > $OUT/chunk.log 2>&1; rc=$?; cat $OUT/chunk.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python tools/stamps_split.py torus:32,32,32 256 1024 7168 32768 > $OUT/stamps_torus.log 2>&1; rc=$?; cat $OUT/stamps_torus.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python tools/stamps_split.py jellyfish:100000,16,1 512 3840 > $OUT/stamps_jf.log 2>&1; rc=$?; cat $OUT/stamps_jf.log; [ $rc -eq 0 ] || exit $rc
+bash tools/sweep_gpu.sh $OUT/sw '|--fabric torus:32,32,32 --steps 3 --warmup 1' 'SDNROUTE_DFS_FLAGS=2|--fabric torus:32,32,32 --steps 3 --warmup 1' \
+  'SDNROUTE_DFS_FLAGS=4|--fabric torus:32,32,32 --steps 3 --warmup 1' \
+  '|--fabric jellyfish:100000,16,1 --steps 2 --warmup 1' 'SDNROUTE_DFS_FLAGS=3|--fabric jellyfish:100000,16,1 --steps 2 --warmup 1' \
+  'SDNROUTE_DFS_FLAGS=5|--fabric jellyfish:100000,16,1 --steps 2 --warmup 1'
