@@ -1110,6 +1110,100 @@ __host__ __device__ inline size_t split_lds_words(int V, int ring, int ns, bool 
 // << 16 (sdnr_dfs_tables_packed), parent | slot << 26 (sdnr_dfs_tables_slots)
 constexpr int kTreeInt32 = 0, kTreePort16 = 1, kTreeSlot = 2;
 
+// The writer wave of the split kernels: drains the NS search waves' record
+// queues (vertex | slot << 26, parent[, depth]) into the table rows, loading
+// the port of each tree edge off the search chain.
+template <int NS, bool HOPS, int PK>
+__device__ __forceinline__ void split_writer(int V, int W, const int32_t *__restrict__ ell_port,
+                                             const uint2 *qrec, const uint32_t *qdep, int *ctl,
+                                             int lane, int32_t *__restrict__ out_parent,
+                                             int32_t *__restrict__ out_port,
+                                             int32_t *__restrict__ out_hops, int *__restrict__ err,
+                                             int flags)
+{
+    constexpr unsigned kIdle = 1u << 26;
+    constexpr bool PACKED = PK != kTreeInt32;
+    int consd[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) consd[k] = 0;
+    unsigned idle = 0;
+    for (;;) {
+        bool any = false, all_done = true;
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            // records first, then the row: a source's row is announced
+            // before its first record, and changes only after the
+            // writer consumed all of the previous source's records
+            const int P = __hip_atomic_load(&ctl[k], __ATOMIC_ACQUIRE,
+                                            __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int row = __hip_atomic_load(&ctl[2 * NS + k], __ATOMIC_ACQUIRE,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int C = consd[k];
+            if (P > C) {
+                any = true;
+                all_done = false;
+                const int n = P - C < SDNR_WAVE ? P - C : SDNR_WAVE;
+                if (lane < n) {
+                    const int at = k * kSplitQ + ((C + lane) & (kSplitQ - 1));
+                    const uint2 r = qrec[at];
+                    const int v = (int)(r.x & 0x3FFFFFFu), slot = (int)(r.x >> 26);
+                    const int par = (int)r.y;
+                    const size_t e = (size_t)row * V + v;
+                    if (PK == kTreeSlot) {     // no port lookup: the slot names it
+                        const int32_t tv = (int32_t)((uint32_t)par | ((uint32_t)slot << 26));
+                        if (flags & kFlagNT) __builtin_nontemporal_store(tv, &out_parent[e]);
+                        else if (!(flags & kFlagNoStore)) out_parent[e] = tv;
+                    } else {
+                        const int pt = (flags & kFlagNoPort) ? slot
+                                                             : ell_port[(size_t)par * W + slot];
+                        if (flags & kFlagNoStore) {
+                            // diagnostic: records consumed, no table stores
+                        } else if (flags & kFlagNT) {
+                            if (PACKED) {
+                                __builtin_nontemporal_store(
+                                    (int32_t)(((uint32_t)par & 0xFFFFu) | ((uint32_t)pt << 16)),
+                                    &out_parent[e]);
+                            } else {
+                                __builtin_nontemporal_store(par, &out_parent[e]);
+                                __builtin_nontemporal_store(pt, &out_port[e]);
+                            }
+                            if (HOPS) __builtin_nontemporal_store((int)qdep[at], &out_hops[e]);
+                        } else {
+                            if (PACKED) {
+                                out_parent[e] = (int32_t)(((uint32_t)par & 0xFFFFu) |
+                                                          ((uint32_t)pt << 16));
+                            } else {
+                                out_parent[e] = par;
+                                out_port[e] = pt;
+                            }
+                            if (HOPS) out_hops[e] = (int)qdep[at];
+                        }
+                    }
+                }
+                consd[k] = C + n;
+                // the record reads above are done (LDS ops in order)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                if (lane == 0) __hip_atomic_store(&ctl[NS + k], C + n, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if (row != -1 ||
+                       __hip_atomic_load(&ctl[k], __ATOMIC_ACQUIRE,
+                                         __HIP_MEMORY_SCOPE_WORKGROUP) != C) {
+                all_done = false;              // running, or published meanwhile
+            }
+        }
+        if (all_done) break;
+        if (any) {
+            idle = 0;
+        } else {
+            if (++idle > kIdle) {
+                if (lane == 0) atomicOr(err, 16);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
 template <int LPR, int J, bool HOPS, int RING, int NS, int FMT, int PK>
 __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
     int V, int W, const void *__restrict__ rows, const uint32_t *__restrict__ rhi,
@@ -1121,7 +1215,6 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
     constexpr int R = 64 / LPR;
     constexpr int K = R * J;
     constexpr unsigned kSpin = 1u << 22;
-    constexpr unsigned kIdle = 1u << 26;
     constexpr bool PACKED = PK != kTreeInt32;
     static_assert(K <= 64, "one stack slot per lane");
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -1371,86 +1464,8 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
         }
 #endif
     } else {
-        // ------------------------------------------------------ the writer
-        int consd[NS];
-#pragma unroll
-        for (int k = 0; k < NS; ++k) consd[k] = 0;
-        unsigned idle = 0;
-        for (;;) {
-            bool any = false, all_done = true;
-#pragma unroll
-            for (int k = 0; k < NS; ++k) {
-                // records first, then the row: a source's row is announced
-                // before its first record, and changes only after the
-                // writer consumed all of the previous source's records
-                const int P = __hip_atomic_load(&ctl[k], __ATOMIC_ACQUIRE,
-                                                __HIP_MEMORY_SCOPE_WORKGROUP);
-                const int row = __hip_atomic_load(&ctl[2 * NS + k], __ATOMIC_ACQUIRE,
-                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-                const int C = consd[k];
-                if (P > C) {
-                    any = true;
-                    all_done = false;
-                    const int n = P - C < SDNR_WAVE ? P - C : SDNR_WAVE;
-                    if (lane < n) {
-                        const int at = k * kSplitQ + ((C + lane) & (kSplitQ - 1));
-                        const uint2 r = qrec[at];
-                        const int v = (int)(r.x & 0x3FFFFFFu), slot = (int)(r.x >> 26);
-                        const int par = (int)r.y;
-                        const size_t e = (size_t)row * V + v;
-                        if (PK == kTreeSlot) {     // no port lookup: the slot names it
-                            const int32_t tv = (int32_t)((uint32_t)par | ((uint32_t)slot << 26));
-                            if (flags & kFlagNT) __builtin_nontemporal_store(tv, &out_parent[e]);
-                            else if (!(flags & kFlagNoStore)) out_parent[e] = tv;
-                        } else {
-                            const int pt = (flags & kFlagNoPort) ? slot
-                                                                 : ell_port[(size_t)par * W + slot];
-                            if (flags & kFlagNoStore) {
-                                // diagnostic: records consumed, no table stores
-                            } else if (flags & kFlagNT) {
-                                if (PACKED) {
-                                    __builtin_nontemporal_store(
-                                        (int32_t)(((uint32_t)par & 0xFFFFu) | ((uint32_t)pt << 16)),
-                                        &out_parent[e]);
-                                } else {
-                                    __builtin_nontemporal_store(par, &out_parent[e]);
-                                    __builtin_nontemporal_store(pt, &out_port[e]);
-                                }
-                                if (HOPS) __builtin_nontemporal_store((int)qdep[at], &out_hops[e]);
-                            } else {
-                                if (PACKED) {
-                                    out_parent[e] = (int32_t)(((uint32_t)par & 0xFFFFu) |
-                                                              ((uint32_t)pt << 16));
-                                } else {
-                                    out_parent[e] = par;
-                                    out_port[e] = pt;
-                                }
-                                if (HOPS) out_hops[e] = (int)qdep[at];
-                            }
-                        }
-                    }
-                    consd[k] = C + n;
-                    // the record reads above are done (LDS ops in order)
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-                    if (lane == 0) __hip_atomic_store(&ctl[NS + k], C + n, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-                } else if (row != -1 ||
-                           __hip_atomic_load(&ctl[k], __ATOMIC_ACQUIRE,
-                                             __HIP_MEMORY_SCOPE_WORKGROUP) != C) {
-                    all_done = false;              // running, or published meanwhile
-                }
-            }
-            if (all_done) break;
-            if (any) {
-                idle = 0;
-            } else {
-                if (++idle > kIdle) {
-                    if (lane == 0) atomicOr(err, 16);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
+        split_writer<NS, HOPS, PK>(V, W, ell_port, qrec, qdep, ctl, lane, out_parent, out_port,
+                                   out_hops, err, flags);
     }
 }
 
@@ -2235,7 +2250,7 @@ static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, in
     do {                                                                                     \
         auto k = dfs_split_kernel<L_, J_, H_, R_, NS, F_, P_>;                               \
         sdnr_allow_lds(reinterpret_cast<const void *>(k), lds);                              \
-        hipLaunchKernelGGL(k, dim3(grid), dim3((NS + 1) * 64), lds, ctx->stream, V, W, rows, \
+        hipLaunchKernelGGL(k, dim3(grid), dim3((NS + 1) * 64), lds, ctx->stream, V, W, rows,     \
                            ctx->ell_hi, ctx->ell_port, d_src, nsrc, par, d_port, d_hops,     \
                            spill, ctx->d_err, flags);                                        \
     } while (0)

@@ -674,20 +674,20 @@ constexpr int kPlVis = 0, kPlFront = 1, kPlNext = 2, kPlDist = 3, kPlSlot = 11;
 __host__ __device__ constexpr int plane_count(int sb) { return sb <= 5 ? 16 : kPlSlot + sb; }
 
 __global__ __launch_bounds__(256) void msbfs_plane_seed_kernel(
-    int V, const int32_t *__restrict__ dst, int ndst, uint64_t *__restrict__ pl, int npl)
+    int V, int VS, const int32_t *__restrict__ dst, int ndst, uint64_t *__restrict__ pl, int npl)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= ndst) return;
     const int d = dst[i];
     if (d < 0 || d >= V) return;
-    uint64_t *b = pl + (size_t)(i >> 6) * npl * V;
-    atomicOr((unsigned long long *)&b[(size_t)kPlVis * V + d], 1ull << (i & 63));
-    atomicOr((unsigned long long *)&b[(size_t)kPlFront * V + d], 1ull << (i & 63));
+    uint64_t *b = pl + (size_t)(i >> 6) * npl * VS;
+    atomicOr((unsigned long long *)&b[(size_t)kPlVis * VS + d], 1ull << (i & 63));
+    atomicOr((unsigned long long *)&b[(size_t)kPlFront * VS + d], 1ull << (i & 63));
 }
 
 template <int SB>
 __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
-    int V, int W, const int32_t *__restrict__ ell_col, int ndst, int lvl, int flip,
+    int V, int VS, int W, const int32_t *__restrict__ ell_col, int ndst, int lvl, int flip,
     uint64_t *__restrict__ pl, int *changed)
 {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
@@ -697,12 +697,12 @@ __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
     if (lvl > 1 && __hip_atomic_load(&changed[lvl - 1], __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT) == 0) return;
     if (x >= V) return;
-    uint64_t *b = pl + (size_t)batch * plane_count(SB) * V;
-    const uint64_t *front = b + (size_t)(flip ? kPlNext : kPlFront) * V;
-    uint64_t *next = b + (size_t)(flip ? kPlFront : kPlNext) * V;
+    uint64_t *b = pl + (size_t)batch * plane_count(SB) * VS;
+    const uint64_t *front = b + (size_t)(flip ? kPlNext : kPlFront) * VS;
+    uint64_t *next = b + (size_t)(flip ? kPlFront : kPlNext) * VS;
     const int nb = min(64, ndst - batch * 64);
     const uint64_t all = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
-    const uint64_t vx = b[(size_t)kPlVis * V + x];
+    const uint64_t vx = b[(size_t)kPlVis * VS + x];
     if ((vx & all) == all) {                   // every destination reached x already
         next[x] = 0ull;
         return;
@@ -735,13 +735,13 @@ __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
     const uint64_t nw = (~vx & all) & ~rem;    // bits reached at this level
     next[x] = nw;
     if (nw) {
-        b[(size_t)kPlVis * V + x] = vx | nw;
+        b[(size_t)kPlVis * VS + x] = vx | nw;
 #pragma unroll
         for (int k = 0; k < 8; ++k)
-            if ((lvl >> k) & 1) b[(size_t)(kPlDist + k) * V + x] |= nw;
+            if ((lvl >> k) & 1) b[(size_t)(kPlDist + k) * VS + x] |= nw;
 #pragma unroll
         for (int k = 0; k < SB; ++k)
-            if (sp[k]) b[(size_t)(kPlSlot + k) * V + x] |= sp[k];
+            if (sp[k]) b[(size_t)(kPlSlot + k) * VS + x] |= sp[k];
         changed[lvl] = 1;
     }
 }
@@ -753,7 +753,7 @@ __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
 // (destination, vertex)
 template <int SB>
 __global__ __launch_bounds__(256) void msbfs_plane_tables_kernel(
-    int V, int W, const int32_t *__restrict__ ell_col, const int32_t *__restrict__ ell_port,
+    int V, int VS, int W, const int32_t *__restrict__ ell_col, const int32_t *__restrict__ ell_port,
     int ndst, const uint64_t *__restrict__ pl, uint16_t *__restrict__ dist,
     int32_t *__restrict__ nh, int32_t *__restrict__ nh_port)
 {
@@ -772,13 +772,13 @@ __global__ __launch_bounds__(256) void msbfs_plane_tables_kernel(
         __syncthreads();
     }
     if (x >= V) return;
-    const uint64_t *b = pl + (size_t)batch * plane_count(SB) * V;
-    const uint64_t vx = b[(size_t)kPlVis * V + x];
+    const uint64_t *b = pl + (size_t)batch * plane_count(SB) * VS;
+    const uint64_t vx = b[(size_t)kPlVis * VS + x];
     uint64_t d[8], s[SB];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) d[k] = b[(size_t)(kPlDist + k) * V + x];
+    for (int k = 0; k < 8; ++k) d[k] = b[(size_t)(kPlDist + k) * VS + x];
 #pragma unroll
-    for (int k = 0; k < SB; ++k) s[k] = b[(size_t)(kPlSlot + k) * V + x];
+    for (int k = 0; k < SB; ++k) s[k] = b[(size_t)(kPlSlot + k) * VS + x];
     const int nb = min(64, ndst - batch * 64);
     for (int i = 0; i < nb; ++i) {
         const size_t row = (size_t)(batch * 64 + i) * V + x;
@@ -821,7 +821,15 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
     const int V = ctx->V, W = ctx->W;
     const int sb = W <= 8 ? 3 : W <= 16 ? 4 : W <= 32 ? 5 : 6;
     const int nbatch = (ndst + 63) / 64;
-    const size_t per_batch = (size_t)plane_count(sb) * V * sizeof(uint64_t);
+    // plane stride VS = V + 64 words: with a power-of-two stride (torus 32^3:
+    // 256 KiB) the 16 plane streams of a vertex block conflict in the memory
+    // channels by a pattern set by where the allocation lands -- 11.4 to 14.0
+    // ms across fresh allocations in one process; 11.9-12.2 ms with the 512-B
+    // pad (tools/bimodal_settings.py).  SDNROUTE_PLANE_PAD
+    // overrides the pad (words).
+    int VS = V + 64;
+    if (const char *f = getenv("SDNROUTE_PLANE_PAD")) VS = V + atoi(f);
+    const size_t per_batch = (size_t)plane_count(sb) * VS * sizeof(uint64_t);
     // batches per chunk: the planes one level sweeps stay inside the 256 MiB
     // Infinity Cache (measured: torus 32^3 14.9 -> 12.8 ms with 64 batches of
     // 4 MiB instead of all 512 at once; the 100k Jellyfish 127 -> 119 ms)
@@ -848,7 +856,7 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
         const int nd = ndst - c0 * 64 < nbc * 64 ? ndst - c0 * 64 : nbc * 64;
         SDNR_HIP(hipMemsetAsync(pl, 0, (size_t)nbc * per_batch, ctx->stream));
         hipLaunchKernelGGL(msbfs_plane_seed_kernel, dim3((nd + 255) / 256), dim3(256), 0,
-                           ctx->stream, V, d_dst + (size_t)c0 * 64, nd, pl, plane_count(sb));
+                           ctx->stream, V, VS, d_dst + (size_t)c0 * 64, nd, pl, plane_count(sb));
         SDNR_HIP(hipGetLastError());
         // levels go out in groups of kGroup with one host check per group
         constexpr int kGroup = 8;
@@ -857,19 +865,19 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
         for (; lvl < 256 && h_changed; ++lvl) {
             if (sb == 3)
                 hipLaunchKernelGGL(msbfs_plane_level_kernel<3>, dim3(gx, nbc), dim3(256), 0,
-                                   ctx->stream, V, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
+                                   ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
                                    changed);
             else if (sb == 4)
                 hipLaunchKernelGGL(msbfs_plane_level_kernel<4>, dim3(gx, nbc), dim3(256), 0,
-                                   ctx->stream, V, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
+                                   ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
                                    changed);
             else if (sb == 5)
                 hipLaunchKernelGGL(msbfs_plane_level_kernel<5>, dim3(gx, nbc), dim3(256), 0,
-                                   ctx->stream, V, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
+                                   ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
                                    changed);
             else
                 hipLaunchKernelGGL(msbfs_plane_level_kernel<6>, dim3(gx, nbc), dim3(256), 0,
-                                   ctx->stream, V, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
+                                   ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
                                    changed);
             SDNR_HIP(hipGetLastError());
             // the first chunk checks every kGroup levels; the next ones queue
@@ -891,20 +899,20 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
         const size_t tl = d_nh ? (size_t)2 * W * 256 * sizeof(int32_t) : 0;
         if (sb == 3)
             hipLaunchKernelGGL(msbfs_plane_tables_kernel<3>, dim3(gx, nbc), dim3(256), tl,
-                               ctx->stream, V, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
+                               ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
                                nhp);
         else if (sb == 4)
             hipLaunchKernelGGL(msbfs_plane_tables_kernel<4>, dim3(gx, nbc), dim3(256), tl,
-                               ctx->stream, V, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
+                               ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
                                nhp);
         else if (sb == 5)
             hipLaunchKernelGGL(msbfs_plane_tables_kernel<5>, dim3(gx, nbc), dim3(256), tl,
-                               ctx->stream, V, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
+                               ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
                                nhp);
         else {
             sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<6>), tl);
             hipLaunchKernelGGL(msbfs_plane_tables_kernel<6>, dim3(gx, nbc), dim3(256), tl,
-                               ctx->stream, V, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
+                               ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
                                nhp);
         }
         SDNR_HIP(hipGetLastError());

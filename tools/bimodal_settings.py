@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """Torus 32^3 shortest tables: the time depends on where the allocation lands
 (tools/bimodal_probe.py: 11.4-14.9 ms across fresh allocations in ONE
-process).  Does a plane chunk below the 256 MiB Infinity Cache remove the
-dependence?  R rounds, each with a different pad before a fresh Context and
-tables; per round the chunk sizes given (batches of 4 MiB of planes) are
-timed back to back, 3 calls each (HIP events on the kernels' stream).
-    python tools/bimodal_chunk.py R chunk [chunk ...]"""
+process).  Which setting removes the dependence?  R rounds, each with a
+different pad before a fresh Context and tables; per round every setting
+given (environment assignments read by the library at each call, e.g.
+SDNROUTE_PLANE_CHUNK=48 or SDNROUTE_PLANE_PAD=64) is timed back to back,
+3 calls each (HIP events on the kernels' stream).
+    python tools/bimodal_chunk.py R NAME=VALUE[,NAME=VALUE] ..."""
 import os
 import sys
 
@@ -19,6 +20,7 @@ from sdnmpi_amd import topologies as T  # noqa: E402
 
 
 def main(R, chunks):
+    base = {k: os.environ.get(k) for c in chunks for k, _ in (a.split("=") for a in c.split(","))}
     dev = torch.device("cuda", 0)
     fab = T.by_name("torus:32,32,32")
     csr = fab.csr()
@@ -40,7 +42,14 @@ def main(R, chunks):
         port = torch.empty((S, V), dtype=torch.int32, device=dev)
         line = []
         for c in chunks:
-            os.environ["SDNROUTE_PLANE_CHUNK"] = str(c)
+            for k, v in base.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+            for a in c.split(","):
+                k, v = a.split("=")
+                os.environ[k] = v
             ctx.shortest_tables_device(srcs.data_ptr(), S, dist.data_ptr(), nh.data_ptr(),
                                        port.data_ptr())
             ts = []
@@ -53,16 +62,15 @@ def main(R, chunks):
                 torch.cuda.synchronize(dev)
                 ts.append(e0.elapsed_time(e1))
             res[c].append(min(ts))
-            line.append("chunk %d: %.2f" % (c, min(ts)))
+            line.append("%s: %.2f" % (c, min(ts)))
         print("round %d: %s" % (r, " | ".join(line)), flush=True)
         ctx.close()
         del dist, nh, port
         torch.cuda.set_stream(torch.cuda.default_stream(dev))
     for c in chunks:
         v = np.array(res[c])
-        print("chunk %3d (%3d MiB of planes): min %.2f median %.2f max %.2f ms" % (
-            c, c * 4, v.min(), np.median(v), v.max()))
+        print("%-40s min %.2f median %.2f max %.2f ms" % (c, v.min(), np.median(v), v.max()))
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]), [int(x) for x in sys.argv[2:]] or [64, 48, 32])
+    main(int(sys.argv[1]), sys.argv[2:] or ["SDNROUTE_PLANE_CHUNK=64", "SDNROUTE_PLANE_CHUNK=32"])
