@@ -1615,11 +1615,15 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
             if (lane == 0) __hip_atomic_store(&ctl[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             int pub = 1, pubd = 1, sp = 1, lo = 0;       // published / announced
             constexpr int NPF = 1;        // rows of the NPF largest children in flight
-            int pu[NPF], xp[NPF];
+            // the prefetched rows stay u16 across the loop back-edge: an int
+            // copy there needs the load's data (s_waitcnt vmcnt(0) at the end
+            // of every push), a u16 one is widened where the row is used
+            int pu[NPF];
+            uint16_t xp[NPF];
 #pragma unroll
             for (int k = 0; k < NPF; ++k) {
                 pu[k] = -1;
-                xp[k] = V;
+                xp[k] = (uint16_t)V;
             }
 #ifdef SDNR_STAMPS
             unsigned long long st_t0, st_t1, st_row = 0, st_cand = 0, st_false = 0, st_bp = 0,
@@ -1677,7 +1681,7 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                 int x = -1;
 #pragma unroll
                 for (int k = 0; k < NPF; ++k)
-                    if (x < 0 && u == pu[k]) x = xp[k];
+                    if (x < 0 && u == pu[k]) x = (int)xp[k];
                 if (x < 0) x = (int)adj[(size_t)u * 64 + lane];
                 const uint32_t wv = vis[x >> 5];
                 const bool fresh = ((wv >> (x & 31)) & 1u) == 0u;
