@@ -2116,12 +2116,20 @@ extern "C" int sdnr_debug_stamps(unsigned long long *out16)
 // work per child is its in-degree -- 3 workers for rows of 33-64 neighbours
 // (k=48: 0.116 ms vs 0.138 with 2), 2 for rows of <= 32 (dragonfly, 23
 // neighbours: 0.289 vs 0.300 ms with 3); SDNROUTE_DFS_ASYNC_WAVES=2..6
-static int dfs_async_waves(const sdnr_ctx *ctx)
+static int dfs_async_waves(const sdnr_ctx *ctx, int nsrc)
 {
     if (const char *f = getenv("SDNROUTE_DFS_ASYNC_WAVES")) {
         const int k = atoi(f);
-        if (k >= 2 && k <= 6) return k;
+        if ((k >= 2 && k <= 6) || k == 8) return k;
     }
+    // at most ~2 sources per CU (one GPU's share of a multi-GPU step, single
+    // sources): 5 decrement workers keep the counts fresher and the search
+    // wave still has its SIMD mostly to itself -- k=48 1 / 144 / 256 / 288
+    // sources 63.4 / 64.3 / 65.1 / 69.1 -> 56.8 / 58.4 / 59.4 / 64.2 us,
+    // dragonfly 258 sources 127.7 -> 120.8 us; equal at 576 sources, and
+    // slower once every CU holds several sources (k=48 1,152: 91.6 -> 137 us
+    // with 4 workers), where the workers compete with the search waves
+    if (nsrc <= 2 * ctx->num_cus) return 6;
     return ctx->max_deg <= 32 ? 3 : 4;
 }
 
@@ -2393,7 +2401,7 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
     const bool coop = !count && coop_ok && (force ? !strcmp(force, "coop") : small);
     if (async) {
         int *err = ctx->d_err;
-        const int nw = dfs_async_waves(ctx);
+        const int nw = dfs_async_waves(ctx, nsrc);
         // workgroups per CU: LDS, and the 32 wave slots; the compact layout
         // (u16 counts, u16 parents + u8 slots) where it holds more sources
         // at once and the full layout cannot hold them all (dragonfly 2,064
@@ -2419,7 +2427,7 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         // workers (dragonfly 0.316 -> 0.300 ms, k=48 unchanged)
         static const char *names[] = {"", "", "dfs_async_kernel<2>", "dfs_async_kernel<3>",
                                       "dfs_async_kernel<4>", "dfs_async_kernel<5>",
-                                      "dfs_async_kernel<6>"};
+                                      "dfs_async_kernel<6>", "", "dfs_async_kernel<8>"};
         ctx->last_kernel = names[nw];
 #define SDNR_ASYNC_P(N_, H_, P_)                                                             \
     do {                                                                                     \
@@ -2437,12 +2445,14 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
                                            "dfs_async_kernel<3,packed>",
                                            "dfs_async_kernel<4,packed>",
                                            "dfs_async_kernel<5,packed>",
-                                           "dfs_async_kernel<6,packed>"};
+                                           "dfs_async_kernel<6,packed>", "",
+                                           "dfs_async_kernel<8,packed>"};
             ctx->last_kernel = pnames[nw];
             if (nw == 2) SDNR_ASYNC_P(2, false, true);
             else if (nw == 3) SDNR_ASYNC_P(3, false, true);
             else if (nw == 5) SDNR_ASYNC_P(5, false, true);
             else if (nw == 6) SDNR_ASYNC_P(6, false, true);
+            else if (nw == 8) SDNR_ASYNC_P(8, false, true);
             else SDNR_ASYNC_P(4, false, true);
         } else if (nw == 2) {
             if (hops) SDNR_ASYNC(2, true); else SDNR_ASYNC(2, false);
@@ -2452,6 +2462,8 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
             if (hops) SDNR_ASYNC(5, true); else SDNR_ASYNC(5, false);
         } else if (nw == 6) {
             if (hops) SDNR_ASYNC(6, true); else SDNR_ASYNC(6, false);
+        } else if (nw == 8) {
+            if (hops) SDNR_ASYNC(8, true); else SDNR_ASYNC(8, false);
         } else {
             if (hops) SDNR_ASYNC(4, true); else SDNR_ASYNC(4, false);
         }

@@ -148,6 +148,24 @@ def test_dfs_packed_fullsize_k48(ctx, monkeypatch, strategy):
     np.testing.assert_array_equal(tree, _pack(po, to))
 
 
+@pytest.mark.parametrize("nsrc", [1, 144, 512, 513])
+def test_dfs_packed_k48_worker_count(ctx, monkeypatch, nsrc):
+    """At most 2 sources per CU (one GPU's share of a multi-GPU step): the
+    async kernel runs 5 decrement workers per source instead of 3
+    (dfs_async_waves); the tables stay bit-exact."""
+    import torch
+    _strategy(monkeypatch, "async")
+    fabric = T.fat_tree(48)
+    csr = fabric.csr()
+    srcs = np.unique(fabric.host_table()[0]).astype(np.int32)[:nsrc]
+    ctx.upload(csr)
+    tree = ctx.dfs_tables_packed(srcs)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    assert ctx.last_kernel() == "dfs_async_kernel<%d,packed>" % (6 if nsrc <= 2 * cus else 4)
+    po, to, _ = O.dfs_tables(csr, srcs, with_hops=False, nthreads=NTHREADS)
+    np.testing.assert_array_equal(tree, _pack(po, to))
+
+
 def _max_runs(csr):
     """Most arithmetic runs a sorted row (out or in) needs -- the encoding of
     capi.hip's encode_runs (strides <= 511)."""
@@ -246,7 +264,7 @@ def test_dfs_dragonfly_one_residency_round(ctx):
 
 
 @pytest.mark.parametrize("c16", ["0", "1"])
-@pytest.mark.parametrize("waves", [2, 3, 4, 5, 6])
+@pytest.mark.parametrize("waves", [2, 3, 4, 5, 6, 8])
 @pytest.mark.parametrize("name", ["fat_tree_k8", "jellyfish_n60_r5", "torus_5x3x2"])
 def test_dfs_packed_async_waves(ctx, monkeypatch, name, waves, c16):
     _strategy(monkeypatch, "async")
@@ -392,6 +410,26 @@ def test_shortest_fullsize_fat_tree(ctx, monkeypatch, strategy):
     if strategy != "msbfs":
         assert ctx.last_kernel().startswith({"auto": "msbfs_plane_level_kernel",
                                              "dest": "bfs_dest_kernel"}[strategy])
+    do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
+    np.testing.assert_array_equal(dist, do)
+    np.testing.assert_array_equal(nh, nho)
+    np.testing.assert_array_equal(nhp, nhpo)
+
+
+@pytest.mark.parametrize("pad", ["0", "1", "64", "1000"])
+@pytest.mark.parametrize("name", ["fat_tree_k8", "torus_5x3x2"])
+def test_shortest_plane_stride_pad(ctx, monkeypatch, name, pad):
+    """The bit-plane BFS with plane strides V + pad (SDNROUTE_PLANE_PAD; 64 is
+    the default), two chunks of batches so the batch stride is
+    exercised too: tables independent of the pad."""
+    monkeypatch.setenv("SDNROUTE_SP_STRATEGY", "plane")
+    monkeypatch.setenv("SDNROUTE_PLANE_PAD", pad)
+    monkeypatch.setenv("SDNROUTE_PLANE_CHUNK", "1")
+    csr = G.Golden(name).fabric().csr()
+    dsts = np.concatenate([np.arange(csr.V), np.arange(csr.V)[::-1]]).astype(np.int32)
+    ctx.upload(csr)
+    dist, nh, nhp = ctx.shortest_tables(dsts)
+    assert ctx.last_kernel().startswith("msbfs_plane_level_kernel")
     do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
     np.testing.assert_array_equal(dist, do)
     np.testing.assert_array_equal(nh, nho)
