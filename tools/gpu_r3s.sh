@@ -1,5 +1,6 @@
 #!/bin/bash
 # round-3: row-prefetch split kernel (dfs_pf_kernel): parity subset, A/B, stamps
+# (dfs_pf_kernel and tools/stamps_pf.py were removed after this measurement: DESIGN.md 4.2)
 OUT=gpurun_out/r3s; mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread \
   -k "(small_all_sources and global) or fullsize_sampled" > $OUT/pytest.log 2>&1

@@ -1,5 +1,6 @@
 #!/bin/bash
 # round-3: row-prefetch split kernel with J-slot windows: parity subset, A/B, stamps of both split
+# (dfs_pf_kernel and tools/stamps_pf.py were removed after this measurement: DESIGN.md 4.2)
 # kernels; Jellyfish / torus store-flag sweep; plane-chunk placement probe
 OUT=gpurun_out/r3t; mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread \
