@@ -31,7 +31,7 @@ ts = torch.from_numpy(srcs).to(dev)
 p = torch.empty((len(srcs), csr.V), dtype=torch.int32, device=dev)
 t = torch.empty_like(p)
 buf = (ctypes.c_ulonglong * 16)()
-for nw in (3, 4, 5):
+for nw in [int(x) for x in os.environ.get("STAMPS_WAVES", "3,4,5").split(",")]:
     os.environ["SDNROUTE_DFS_ASYNC_WAVES"] = str(nw)
     for rep in range(2):
         L.sdnr_debug_stamps(buf)
