@@ -329,6 +329,30 @@ def test_route_entries_match_reference(monkeypatch, name, walk):
 
 
 @pytest.mark.gpu
+def test_route_entries_k48_many_pairs(monkeypatch):
+    """65,536 random k=48 host pairs (paths of ~70 entries, some pairs on one
+    switch): the packed 16-lane jump kernel emits the same entries as the
+    one-lane-per-pair serial walk."""
+    from sdnmpi_amd import topologies as T
+    fabric = T.fat_tree(48)
+    db = fabric.populate(TopologyDB())
+    macs = fabric.host_macs()
+    rng = np.random.default_rng(7)
+    a = rng.integers(0, len(macs), 65536)
+    b = np.where(rng.random(65536) < 0.01, a, rng.integers(0, len(macs), 65536))
+    pairs = [(macs[int(x)], macs[int(y)]) for x, y in zip(a, b)]
+    monkeypatch.setenv("SDNROUTE_ROUTE_WALK", "serial")
+    o0, d0, p0 = db.route_entries(pairs)
+    assert db.engine.ctx.last_kernel() == "route_walk_kernel"
+    monkeypatch.delenv("SDNROUTE_ROUTE_WALK")
+    o1, d1, p1 = db.route_entries(pairs)
+    assert db.engine.ctx.last_kernel() == "route_jump_packed_kernel<16>"
+    np.testing.assert_array_equal(o0, o1)
+    np.testing.assert_array_equal(d0, d1)
+    np.testing.assert_array_equal(p0, p1)
+
+
+@pytest.mark.gpu
 def test_route_entries_k48_golden_pairs():
     g = G.Golden("fat_tree_k48_sample")
     fabric = g.fabric()
