@@ -106,6 +106,7 @@ static void free_graph(sdnr_ctx *c)
     c->radj16 = nullptr;
     c->deg32 = nullptr;
     c->radj_owned = false;
+    c->radj_pair = false;
     c->V = -1;
     c->E = 0;
     c->W = 0;
@@ -473,8 +474,16 @@ static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *
         if (he == hipSuccess && maxin <= SDNR_WAVE && dummy + SDNR_WAVE <= 0xFFFF) {
             std::vector<uint16_t> w16(r16.size());
             const std::vector<uint16_t> &src16 = sym ? a16 : r16;
+            // rows of <= 32 in-neighbours: lanes 32..63 repeat lanes 0..31 (the
+            // dummies stay per lane), so a worker pairs two children per load
+            const bool pair = maxin <= SDNR_WAVE / 2;
+            const char *pe = getenv("SDNROUTE_DFS_PAIR");          // 0: off (A/B)
+            ctx->radj_pair = pair && !(pe && !strcmp(pe, "0"));
+            auto at = [&](size_t i) {
+                return ctx->radj_pair ? (i & ~(size_t)(SDNR_WAVE / 2)) : i;   // lane l -> l & 31
+            };
             for (size_t i = 0; i < w16.size(); ++i) {
-                const int x = src16[i];
+                const int x = src16[at(i)];
                 w16[i] = (uint16_t)(x == V ? (int)(dummy + i % SDNR_WAVE) : (x ^ ((x >> 3) & 31)));
             }
             he = hipMalloc(reinterpret_cast<void **>(&ctx->radjw), w16.size() * 2);
@@ -487,7 +496,7 @@ static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *
             const size_t dummyc = ((((size_t)V + 2) >> 1) + 31) & ~(size_t)31;
             if (he == hipSuccess && 2 * (dummyc + SDNR_WAVE) <= 0xFFFF) {
                 for (size_t i = 0; i < w16.size(); ++i) {
-                    const int x = src16[i];
+                    const int x = src16[at(i)];
                     const int h = x >> 1;
                     w16[i] = (uint16_t)(x == V ? (int)(2 * (dummyc + i % SDNR_WAVE))
                                                : ((h ^ ((h >> 3) & 31)) << 1) | (x & 1));

@@ -61,6 +61,9 @@ struct sdnr_ctx {
     uint16_t *radjw = nullptr;          // radj16 as swizzled count indices (async DFS workers)
     uint16_t *radjc = nullptr;          // ... for the compact-LDS form (word << 1 | half)
     bool radj_owned = false;
+    // in-degree <= 32: the pre-swizzled rows (radjw / radjc) repeat their 32
+    // entries in lanes 32..63, so one 64-lane load + ds_sub covers 2 children
+    bool radj_pair = false;
     // out-rows as arithmetic runs (dfs_runs.hip): (V+1) rows x runs_R words
     // of start | stride << 16 | count << 25
     uint32_t *runs = nullptr;

@@ -1060,6 +1060,8 @@ constexpr int kSplitQ = 64;                    // queued records per search wave
 constexpr int kFlagPrio = 1, kFlagNT = 2, kFlagNoStore = 4, kFlagNoPort = 8;
 // dfs_async_kernel: the worker rows are pre-swizzled count indices (radjw)
 constexpr int kFlagPreSwz = 16;
+// ... and pair two children per 64-lane load / ds_sub (in-degree <= 32)
+constexpr int kFlagPairRows = 32;
 
 template <int FMT>
 __device__ __forceinline__ int split_row(const void *__restrict__ rows,
@@ -1806,6 +1808,28 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                 spin = 0;
                 const int n = (P - j + S - 1) / S < G ? (P - j + S - 1) / S : G;
                 const int mine = lane < n ? (int)ring[(j + lane * S) & (RING - 1)] : V;
+                if (flags & kFlagPairRows) {
+                    // rows repeat in lanes 32..63: load g serves child 2g in
+                    // lanes 0..31 and child 2g + 1 in lanes 32..63
+                    constexpr int G2 = G / 2;
+                    const int hiw = lane >> 5;
+                    int r[G2];
+#pragma unroll
+                    for (int g = 0; g < G2; ++g) {
+                        const int ca = read_lane(mine, 2 * g), cb = read_lane(mine, 2 * g + 1);
+                        r[g] = radj[(size_t)(hiw ? cb : ca) * 64 + lane];
+                    }
+#pragma unroll
+                    for (int g = 0; g < G2; ++g)
+                        if (2 * g + hiw < n) {
+                            if (C16) atomicSub(&cnt[r[g] >> 1], 1u << ((r[g] & 1) << 4));
+                            else atomicSub(&cnt[r[g]], 1u);
+                        }
+                    j += n * S;
+                    if (lane == 0) __hip_atomic_store(&ctl[2 + w - 1], j, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                    continue;
+                }
                 int r[G];
                 // unconditional: a slot past n loads the sentinel row V (L2
                 // resident); guarding each load measured 20 % slower
@@ -2420,7 +2444,8 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         const char *pz = getenv("SDNROUTE_DFS_PRESWZ");
         const uint16_t *rw = c16 ? ctx->radjc : ctx->radjw;
         const bool preswz = rw && !(pz && !strcmp(pz, "0"));
-        const int aflags = dfs_flags(kFlagPrio) | (preswz ? kFlagPreSwz : 0);
+        const int aflags = dfs_flags(kFlagPrio) | (preswz ? kFlagPreSwz : 0) |
+                           (preswz && ctx->radj_pair ? kFlagPairRows : 0);
         int cgrid = (int)((size_t)ctx->num_cus * cpc);
         if (cgrid > nsrc) cgrid = nsrc;
         // the search wave issues at raised priority over the decrement
