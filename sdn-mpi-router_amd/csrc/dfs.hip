@@ -1060,8 +1060,6 @@ constexpr int kSplitQ = 64;                    // queued records per search wave
 constexpr int kFlagPrio = 1, kFlagNT = 2, kFlagNoStore = 4, kFlagNoPort = 8;
 // dfs_async_kernel: the worker rows are pre-swizzled count indices (radjw)
 constexpr int kFlagPreSwz = 16;
-// ... and pair two children per 64-lane load / ds_sub (in-degree <= 32)
-constexpr int kFlagPairRows = 32;
 
 template <int FMT>
 __device__ __forceinline__ int split_row(const void *__restrict__ rows,
@@ -1491,7 +1489,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int swz(int x) { return lds_swz(x); }   // common.h
 
-template <int NW, bool HOPS, bool PACKED, bool C16>
+template <int NW, bool HOPS, bool PACKED, bool C16, bool PAIR>
 __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
     int V, const uint16_t *__restrict__ adj, const uint16_t *__restrict__ radj,
     const uint32_t *__restrict__ deg, const int32_t *__restrict__ row_ptr,
@@ -1808,9 +1806,11 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                 spin = 0;
                 const int n = (P - j + S - 1) / S < G ? (P - j + S - 1) / S : G;
                 const int mine = lane < n ? (int)ring[(j + lane * S) & (RING - 1)] : V;
-                if (flags & kFlagPairRows) {
+                if constexpr (PAIR) {
                     // rows repeat in lanes 32..63: load g serves child 2g in
-                    // lanes 0..31 and child 2g + 1 in lanes 32..63
+                    // lanes 0..31 and child 2g + 1 in lanes 32..63 (a template
+                    // case: a runtime branch here cost the unpaired k=48
+                    // kernel 3 %)
                     constexpr int G2 = G / 2;
                     const int hiw = lane >> 5;
                     int r[G2];
@@ -2444,8 +2444,9 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         const char *pz = getenv("SDNROUTE_DFS_PRESWZ");
         const uint16_t *rw = c16 ? ctx->radjc : ctx->radjw;
         const bool preswz = rw && !(pz && !strcmp(pz, "0"));
-        const int aflags = dfs_flags(kFlagPrio) | (preswz ? kFlagPreSwz : 0) |
-                           (preswz && ctx->radj_pair ? kFlagPairRows : 0);
+        const int aflags = dfs_flags(kFlagPrio) | (preswz ? kFlagPreSwz : 0);
+        // paired worker rows (in-degree <= 32, pre-swizzled rows only)
+        const bool pair = preswz && ctx->radj_pair;
         int cgrid = (int)((size_t)ctx->num_cus * cpc);
         if (cgrid > nsrc) cgrid = nsrc;
         // the search wave issues at raised priority over the decrement
@@ -2456,7 +2457,10 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         ctx->last_kernel = names[nw];
 #define SDNR_ASYNC_P(N_, H_, P_)                                                             \
     do {                                                                                     \
-        auto k = c16 ? dfs_async_kernel<N_, H_, P_, true> : dfs_async_kernel<N_, H_, P_, false>; \
+        auto k = c16 ? (pair ? dfs_async_kernel<N_, H_, P_, true, true>                      \
+                             : dfs_async_kernel<N_, H_, P_, true, false>)                    \
+                     : (pair ? dfs_async_kernel<N_, H_, P_, false, true>                     \
+                             : dfs_async_kernel<N_, H_, P_, false, false>);                  \
         allow_full_lds(k);                                                                   \
         hipLaunchKernelGGL(k, dim3(cgrid), dim3(N_ * 64), cl, ctx->stream, V, ctx->adj16,    \
                            preswz ? rw : ctx->radj16, ctx->deg32, ctx->row_ptr,              \
