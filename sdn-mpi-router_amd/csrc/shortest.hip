@@ -685,10 +685,19 @@ __global__ __launch_bounds__(256) void msbfs_plane_seed_kernel(
     atomicOr((unsigned long long *)&b[(size_t)kPlFront * VS + d], 1ull << (i & 63));
 }
 
+// A busy level is a chain of dependent L2 round trips per thread -- visited
+// word, row, frontier gathers, then a read-modify-write of the level / slot
+// planes.  opt kPlAtomicOr: the plane updates are return-less atomic ORs
+// performed in L2 (each (batch, x) word has one writer), so the wave does not
+// wait for the old plane values -- 3.5 % off the k=48 and dragonfly steps,
+// 7 % slower on the torus, so small graphs only.  (Row loads
+// issued beside the visited load were slower on every fabric.)
+constexpr int kPlAtomicOr = 2;
+
 template <int SB>
 __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
     int V, int VS, int W, const int32_t *__restrict__ ell_col, int ndst, int lvl, int flip,
-    uint64_t *__restrict__ pl, int *changed)
+    uint64_t *__restrict__ pl, int *changed, int opt)
 {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int batch = blockIdx.y;
@@ -736,12 +745,22 @@ __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
     next[x] = nw;
     if (nw) {
         b[(size_t)kPlVis * VS + x] = vx | nw;
+        if (opt & kPlAtomicOr) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-            if ((lvl >> k) & 1) b[(size_t)(kPlDist + k) * VS + x] |= nw;
+            for (int k = 0; k < 8; ++k)
+                if ((lvl >> k) & 1)
+                    atomicOr((unsigned long long *)&b[(size_t)(kPlDist + k) * VS + x], nw);
 #pragma unroll
-        for (int k = 0; k < SB; ++k)
-            if (sp[k]) b[(size_t)(kPlSlot + k) * VS + x] |= sp[k];
+            for (int k = 0; k < SB; ++k)
+                if (sp[k]) atomicOr((unsigned long long *)&b[(size_t)(kPlSlot + k) * VS + x], sp[k]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if ((lvl >> k) & 1) b[(size_t)(kPlDist + k) * VS + x] |= nw;
+#pragma unroll
+            for (int k = 0; k < SB; ++k)
+                if (sp[k]) b[(size_t)(kPlSlot + k) * VS + x] |= sp[k];
+        }
         changed[lvl] = 1;
     }
 }
@@ -849,6 +868,10 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
     int *changed = reinterpret_cast<int *>(reinterpret_cast<char *>(ctx->scratch) +
                                            (size_t)cb * per_batch);   // [256] per level
     const int gx = (V + 255) / 256;
+    // level-pass options: kPlAtomicOr up to 16k vertices (k=48, dragonfly);
+    // SDNROUTE_PLANE_OPT=0|2 overrides
+    int popt = V <= 16384 ? kPlAtomicOr : 0;
+    if (const char *f = getenv("SDNROUTE_PLANE_OPT")) popt = atoi(f) & kPlAtomicOr;
     int levels = 0;
     int guess = 0;                               // levels of the previous chunk
     for (int c0 = 0; c0 < nbatch; c0 += cb) {
@@ -866,19 +889,19 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
             if (sb == 3)
                 hipLaunchKernelGGL(msbfs_plane_level_kernel<3>, dim3(gx, nbc), dim3(256), 0,
                                    ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
-                                   changed);
+                                   changed, popt);
             else if (sb == 4)
                 hipLaunchKernelGGL(msbfs_plane_level_kernel<4>, dim3(gx, nbc), dim3(256), 0,
                                    ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
-                                   changed);
+                                   changed, popt);
             else if (sb == 5)
                 hipLaunchKernelGGL(msbfs_plane_level_kernel<5>, dim3(gx, nbc), dim3(256), 0,
                                    ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
-                                   changed);
+                                   changed, popt);
             else
                 hipLaunchKernelGGL(msbfs_plane_level_kernel<6>, dim3(gx, nbc), dim3(256), 0,
                                    ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
-                                   changed);
+                                   changed, popt);
             SDNR_HIP(hipGetLastError());
             // the first chunk checks every kGroup levels; the next ones queue
             // as many levels as it needed before their first check

@@ -356,12 +356,16 @@ def test_dfs_fullsize_tree_properties(ctx):
             assert k < hi and csr.col[k] == v and csr.port[k] == t[s, v]
 
 
-@pytest.mark.parametrize("strategy", ["auto", "msbfs", "lanes", "lanes-csr", "plane"])
+@pytest.mark.parametrize("strategy", ["auto", "msbfs", "lanes", "lanes-csr", "plane",
+                                      "plane-opt0", "plane-opt2"])
 @pytest.mark.parametrize("name", G.SMALL)
 def test_shortest_small_all_destinations(ctx, monkeypatch, name, strategy):
     if strategy == "lanes-csr":                  # no ELL copy: 64-wide rows + CSR ports
         monkeypatch.setenv("SDNROUTE_ELL", "0")
         strategy = "lanes"
+    if strategy.startswith("plane-opt"):         # plane updates: read-modify-write / atomic OR
+        monkeypatch.setenv("SDNROUTE_PLANE_OPT", strategy[-1])
+        strategy = "plane"
     if strategy != "auto":
         monkeypatch.setenv("SDNROUTE_SP_STRATEGY", strategy)
     fabric = G.Golden(name).fabric()
@@ -396,10 +400,14 @@ def test_shortest_matches_reference_multiple(ctx, name):
             assert [int(csr.dpids[x]) for x in q] == [x for x, _ in w]
 
 
-@pytest.mark.parametrize("strategy", ["auto", "dest", "msbfs"])
+@pytest.mark.parametrize("strategy", ["auto", "dest", "msbfs", "opt0"])
 def test_shortest_fullsize_fat_tree(ctx, monkeypatch, strategy):
-    """k=48: rows of 48 slots -- the bit-plane BFS with 6 slot planes (auto),
-    the per-destination BFS and the level + next-hop kernels."""
+    """k=48: rows of 48 slots -- the bit-plane BFS with 6 slot planes (auto:
+    plane updates by atomic OR; opt0: by read-modify-write), the
+    per-destination BFS and the level + next-hop kernels."""
+    if strategy == "opt0":
+        monkeypatch.setenv("SDNROUTE_PLANE_OPT", "0")
+        strategy = "auto"
     if strategy != "auto":
         monkeypatch.setenv("SDNROUTE_SP_STRATEGY", strategy)
     fabric = T.fat_tree(48)
