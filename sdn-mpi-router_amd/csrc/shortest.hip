@@ -776,7 +776,11 @@ __global__ __launch_bounds__(256) void msbfs_plane_tables_kernel(
     int ndst, const uint64_t *__restrict__ pl, uint16_t *__restrict__ dist,
     int32_t *__restrict__ nh, int32_t *__restrict__ nh_port)
 {
-    extern __shared__ int32_t lrow[];          // [2][W][256]: ids, ports
+    // [2][W][kTabStride]: ids, ports; the odd stride keeps the transposing
+    // stores below conflict-free (with 256, a wave's 64 stores -- slots j,
+    // j+1, ... of one or two vertices -- fell in one or two banks)
+    constexpr int kTabStride = 257;
+    extern __shared__ int32_t lrow[];
     const int x0 = blockIdx.x * blockDim.x;
     const int t = threadIdx.x;
     const int x = x0 + t;
@@ -785,8 +789,8 @@ __global__ __launch_bounds__(256) void msbfs_plane_tables_kernel(
     if (nh) {
         for (int e = t; e < nx * W; e += 256) {   // coalesced reads of the block's rows
             const int xl = e / W, j = e - xl * W;
-            lrow[j * 256 + xl] = ell_col[(size_t)x0 * W + e];
-            lrow[(W + j) * 256 + xl] = ell_port[(size_t)x0 * W + e];
+            lrow[j * kTabStride + xl] = ell_col[(size_t)x0 * W + e];
+            lrow[(W + j) * kTabStride + xl] = ell_port[(size_t)x0 * W + e];
         }
         __syncthreads();
     }
@@ -799,26 +803,48 @@ __global__ __launch_bounds__(256) void msbfs_plane_tables_kernel(
 #pragma unroll
     for (int k = 0; k < SB; ++k) s[k] = b[(size_t)(kPlSlot + k) * VS + x];
     const int nb = min(64, ndst - batch * 64);
-    for (int i = 0; i < nb; ++i) {
-        const size_t row = (size_t)(batch * 64 + i) * V + x;
-        uint32_t L = 0xFFFFu;
-        int best = -1, bport = -1;
-        if ((vx >> i) & 1ull) {
-            L = 0;
+    // 8 destinations at a time: the planes shifted once per group (32-bit
+    // bit extracts after that), the group's 16 LDS lookups issued together
+    // before its stores, instead of one dependent lookup per destination
+    constexpr int CG = 8;
+    for (int i0 = 0; i0 < nb; i0 += CG) {
+        const uint32_t vv = (uint32_t)(vx >> i0);
+        uint32_t dv[8], sv[SB];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) L |= (uint32_t)((d[k] >> i) & 1ull) << k;
-            if (L && nh) {
-                int sl = 0;
+        for (int k = 0; k < 8; ++k) dv[k] = (uint32_t)(d[k] >> i0);
 #pragma unroll
-                for (int k = 0; k < SB; ++k) sl |= (int)((s[k] >> i) & 1ull) << k;
-                best = lrow[sl * 256 + t];
-                bport = lrow[(W + sl) * 256 + t];
+        for (int k = 0; k < SB; ++k) sv[k] = (uint32_t)(s[k] >> i0);
+        uint32_t L[CG];
+        int best[CG], bport[CG];
+#pragma unroll
+        for (int u = 0; u < CG; ++u) {
+            L[u] = 0xFFFFu;
+            best[u] = -1;
+            bport[u] = -1;
+            if ((vv >> u) & 1u) {
+                uint32_t l = 0;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) l |= ((dv[k] >> u) & 1u) << k;
+                L[u] = l;
+                if (l && nh) {
+                    int sl = 0;
+#pragma unroll
+                    for (int k = 0; k < SB; ++k) sl |= (int)((sv[k] >> u) & 1u) << k;
+                    best[u] = lrow[sl * kTabStride + t];
+                    bport[u] = lrow[(W + sl) * kTabStride + t];
+                }
             }
         }
-        dist[row] = (uint16_t)L;
-        if (nh) {
-            nh[row] = best;
-            nh_port[row] = bport;
+#pragma unroll
+        for (int u = 0; u < CG; ++u) {
+            if (i0 + u < nb) {
+                const size_t row = (size_t)(batch * 64 + i0 + u) * V + x;
+                dist[row] = (uint16_t)L[u];
+                if (nh) {
+                    nh[row] = best[u];
+                    nh_port[row] = bport[u];
+                }
+            }
         }
     }
 }
@@ -919,7 +945,7 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
         uint16_t *dist = d_dist + (size_t)c0 * 64 * V;
         int32_t *nh = d_nh ? d_nh + (size_t)c0 * 64 * V : nullptr;
         int32_t *nhp = d_nh_port ? d_nh_port + (size_t)c0 * 64 * V : nullptr;
-        const size_t tl = d_nh ? (size_t)2 * W * 256 * sizeof(int32_t) : 0;
+        const size_t tl = d_nh ? (size_t)2 * W * 257 * sizeof(int32_t) : 0;   // kTabStride
         if (sb == 3)
             hipLaunchKernelGGL(msbfs_plane_tables_kernel<3>, dim3(gx, nbc), dim3(256), tl,
                                ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
@@ -928,10 +954,13 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
             hipLaunchKernelGGL(msbfs_plane_tables_kernel<4>, dim3(gx, nbc), dim3(256), tl,
                                ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
                                nhp);
-        else if (sb == 5)
+        else if (sb == 5) {
+            if (tl > 65536)   // W = 32 with the padded stride
+                sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<5>), tl);
             hipLaunchKernelGGL(msbfs_plane_tables_kernel<5>, dim3(gx, nbc), dim3(256), tl,
                                ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
                                nhp);
+        }
         else {
             sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<6>), tl);
             hipLaunchKernelGGL(msbfs_plane_tables_kernel<6>, dim3(gx, nbc), dim3(256), tl,
