@@ -550,6 +550,7 @@ static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *
     ctx->V = V;
     ctx->E = E;
     ctx->W = W;
+    ctx->plane_depth = 0;
     ctx->max_deg = maxdeg;
     ctx->max_indeg = max_indeg;
     ctx->port16 = port16;

@@ -84,6 +84,7 @@ struct sdnr_ctx {
     bool timed = false;
     const char *last_kernel = "";       // variant launched by the last table call
     int32_t last_launches = 0;          // main-kernel launches of the last table call
+    int32_t plane_depth = 0;            // levels the bit-plane BFS last needed on this graph
     int *d_err = nullptr;               // kernel watchdog word (0 = ok)
     int *h_flag = nullptr;              // pinned host words for level-loop checks
     hipEvent_t ev_flag = nullptr;       // ... and the event the host spins on

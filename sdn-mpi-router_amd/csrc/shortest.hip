@@ -899,7 +899,13 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
     int popt = V <= 16384 ? kPlAtomicOr : 0;
     if (const char *f = getenv("SDNROUTE_PLANE_OPT")) popt = atoi(f) & kPlAtomicOr;
     int levels = 0;
-    int guess = 0;                               // levels of the previous chunk
+    // levels to queue before the first host check: what the previous call
+    // on this graph needed (k=48: 5 launches instead of a group of 8, each
+    // empty level still ~4.5 us), then what the previous chunk needed; a
+    // guess that is too small only costs a further check
+    const char *gq = getenv("SDNROUTE_PLANE_GUESS");   // 0: check every kGroup levels
+    const bool noguess = gq && !strcmp(gq, "0");
+    int guess = noguess ? 0 : ctx->plane_depth;
     for (int c0 = 0; c0 < nbatch; c0 += cb) {
         const int nbc = nbatch - c0 < cb ? nbatch - c0 : cb;
         const int nd = ndst - c0 * 64 < nbc * 64 ? ndst - c0 * 64 : nbc * 64;
@@ -939,9 +945,25 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
         // lvl - 1 levels were queued; those after the last change returned
         // at once
         levels += lvl - 1;
-        guess = lvl < 255 ? lvl : 0;
-        if (const char *f = getenv("SDNROUTE_PLANE_GUESS"))   // 0: check every kGroup levels
-            if (!strcmp(f, "0")) guess = 0;
+        // the first level that reached nothing (every later one is empty
+        // too): the level of the final check when that was the guess,
+        // else found by reading the flags back from there
+        int last0 = lvl - 1;
+        if (!(guess > 0 && last0 == guess)) {
+            for (int hi = last0; hi >= 1;) {
+                const int n = hi < 4 ? hi : 4, st = hi - n + 1;
+                int fl[4];
+                if ((rc = sdnr_fetch_ints(ctx, changed + st, n, fl))) return rc;
+                int k = n - 1;
+                while (k >= 0 && fl[k] == 0) --k;
+                last0 = st + k + 1;
+                if (k >= 0) break;
+                hi = st - 1;
+            }
+        }
+        guess = last0 < 255 ? last0 : 0;
+        if (c0 == 0) ctx->plane_depth = guess;
+        if (noguess) guess = 0;
         uint16_t *dist = d_dist + (size_t)c0 * 64 * V;
         int32_t *nh = d_nh ? d_nh + (size_t)c0 * 64 * V : nullptr;
         int32_t *nhp = d_nh_port ? d_nh_port + (size_t)c0 * 64 * V : nullptr;

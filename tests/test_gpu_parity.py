@@ -424,6 +424,38 @@ def test_shortest_fullsize_fat_tree(ctx, monkeypatch, strategy):
     np.testing.assert_array_equal(nhp, nhpo)
 
 
+@pytest.mark.parametrize("guess", ["default", "0"])
+def test_shortest_plane_depth_cache(ctx, monkeypatch, guess):
+    """The bit-plane BFS queues as many levels as the previous call on the
+    graph needed before its first host check (SDNROUTE_PLANE_GUESS=0: a
+    check every 8 levels).  Calls whose destinations need fewer, then more
+    levels than the cached depth, on one context, against the oracle; and a
+    repeated k=48 call launches only the levels it needs (5, not 8)."""
+    monkeypatch.setenv("SDNROUTE_SP_STRATEGY", "plane")
+    if guess == "0":
+        monkeypatch.setenv("SDNROUTE_PLANE_GUESS", "0")
+    csr = T.torus3d(40, 3, 1).csr()                 # eccentricity 21 from every vertex
+    ctx.upload(csr)
+    for dsts in (np.arange(0, csr.V, 5), np.arange(3), np.arange(csr.V)[::-1], np.arange(70)):
+        dsts = dsts.astype(np.int32)
+        dist, nh, nhp = ctx.shortest_tables(dsts)
+        do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
+        np.testing.assert_array_equal(dist, do)
+        np.testing.assert_array_equal(nh, nho)
+        np.testing.assert_array_equal(nhp, nhpo)
+    fabric = T.fat_tree(48)
+    csr = fabric.csr()
+    dsts = np.unique(fabric.host_table()[0]).astype(np.int32)
+    ctx.upload(csr)
+    ctx.shortest_tables(dsts)
+    first = ctx.last_launches()
+    dist, nh, nhp = ctx.shortest_tables(dsts)
+    assert ctx.last_launches() == (first if guess == "0" else 5)
+    do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
+    np.testing.assert_array_equal(dist, do)
+    np.testing.assert_array_equal(nh, nho)
+
+
 @pytest.mark.parametrize("pad", ["0", "1", "64", "1000"])
 @pytest.mark.parametrize("name", ["fat_tree_k8", "torus_5x3x2"])
 def test_shortest_plane_stride_pad(ctx, monkeypatch, name, pad):
