@@ -909,13 +909,17 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
     for (int c0 = 0; c0 < nbatch; c0 += cb) {
         const int nbc = nbatch - c0 < cb ? nbatch - c0 : cb;
         const int nd = ndst - c0 * 64 < nbc * 64 ? ndst - c0 * 64 : nbc * 64;
-        SDNR_HIP(hipMemsetAsync(pl, 0, (size_t)nbc * per_batch, ctx->stream));
+        // a full chunk's planes end where the level flags begin: one fill
+        // for both (one launch fewer per chunk)
+        const bool full = nbc == cb;
+        SDNR_HIP(hipMemsetAsync(pl, 0, (size_t)nbc * per_batch + (full ? 256 * sizeof(int) : 0),
+                                ctx->stream));
         hipLaunchKernelGGL(msbfs_plane_seed_kernel, dim3((nd + 255) / 256), dim3(256), 0,
                            ctx->stream, V, VS, d_dst + (size_t)c0 * 64, nd, pl, plane_count(sb));
         SDNR_HIP(hipGetLastError());
         // levels go out in groups of kGroup with one host check per group
         constexpr int kGroup = 8;
-        SDNR_HIP(hipMemsetAsync(changed, 0, 256 * sizeof(int), ctx->stream));
+        if (!full) SDNR_HIP(hipMemsetAsync(changed, 0, 256 * sizeof(int), ctx->stream));
         int h_changed = 1, lvl = 1;
         for (; lvl < 256 && h_changed; ++lvl) {
             if (sb == 3)
