@@ -366,52 +366,6 @@ __global__ __launch_bounds__(128) void minplus_square64_kernel(int Vp, uint16_t 
     if (lane_id() == 0) atomicMax(reinterpret_cast<unsigned *>(changed) + 1, mx);
 }
 
-// One-edge relaxation check: D is the exact distance matrix once no entry
-// improves by extending a path with one more edge (min over in-neighbours k
-// of j of D[i][k] + 1 is never below D[i][j]) -- by induction on path
-// length.  After s squarings D is exact up to 2^s hops and INF beyond, so
-// when the largest finite distance M reaches 2^s the squaring loop used to
-// run one more full V^3 pass just to see nothing change; this check costs
-// V^2 x in-degree LDS reads instead.  Each thread owns a column j (its
-// in-row packed in registers), each block a chunk of rows, staged one at a
-// time in LDS.
-__global__ __launch_bounds__(256) void apsp_relax_kernel(int V, int Vp, int maxd,
-                                                         const uint16_t *__restrict__ radj,
-                                                         int rows, const uint16_t *__restrict__ D,
-                                                         int *__restrict__ changed)
-{
-    extern __shared__ uint32_t lrow32[];         // D[i][0..Vp) as u16 pairs
-    const uint16_t *lrow = reinterpret_cast<const uint16_t *>(lrow32);
-    const int j = blockIdx.x * 256 + threadIdx.x;
-    const int i0 = blockIdx.y * rows;
-    const int i1 = min(V, i0 + rows);
-    uint32_t nb[32];                             // in-row of j, sentinel V
-    const uint32_t *rr = reinterpret_cast<const uint32_t *>(radj + (size_t)(j < V ? j : V) * 64);
-#pragma unroll
-    for (int q = 0; q < 32; ++q) nb[q] = rr[q];
-    bool ch = false;
-    for (int i = i0; i < i1; ++i) {
-        __syncthreads();
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(D + (size_t)i * Vp);
-        for (int q = threadIdx.x; q < Vp / 2; q += 256) lrow32[q] = src[q];
-        __syncthreads();
-        if (j < V) {
-            const uint32_t cur = lrow[j];
-            uint32_t best = cur;
-#pragma unroll
-            for (int q = 0; q < 32; ++q) {
-                if (2 * q < maxd) {              // wave-uniform: rows hold <= maxd entries
-                    const uint32_t a = nb[q] & 0xFFFFu, b = nb[q] >> 16;
-                    if (a < (uint32_t)V) best = min(best, (uint32_t)lrow[a] + 1u);
-                    if (b < (uint32_t)V) best = min(best, (uint32_t)lrow[b] + 1u);
-                }
-            }
-            ch |= best < cur;                    // INF + 1 never wins
-        }
-    }
-    if (__ballot(ch) && lane_id() == 0) atomicOr(changed, 1);
-}
-
 }  // namespace
 
 static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp, int mt)
@@ -427,9 +381,6 @@ static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp, int m
     // every distance <= 2^s) the largest finite distance M is < 2^s: no pair
     // is at distance M + 1 <= 2^s, so none is farther
     const int nt = Vp / mt;
-    constexpr int kRelaxRows = 16;
-    const char *rf = getenv("SDNROUTE_APSP_RELAX");
-    const bool relax = ctx->radj16 && ctx->max_indeg <= 64 && !(rf && !strcmp(rf, "0"));
     ctx->last_launches = 0;
     for (int it = 1; it <= 40; ++it) {         // 2^40 >> any hop distance
         ctx->last_launches = it;
@@ -442,23 +393,9 @@ static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp, int m
                                D, changed);
         SDNR_HIP(hipGetLastError());
         int h[2] = {0, 0};
-        int rc = sdnr_fetch_ints(ctx, changed, 2, h);
+        const int rc = sdnr_fetch_ints(ctx, changed, 2, h);
         if (rc) return rc;
         if (!h[0] || (it < 31 && (long long)h[1] < (1ll << it))) break;
-        // M reached the 2^s horizon: a one-edge relaxation (V^2 x in-degree)
-        // settles whether D is already exact instead of another V^3 pass
-        // (k=48: 2 squarings + checks instead of 3 squarings);
-        // SDNROUTE_APSP_RELAX=0 keeps squaring
-        if (relax) {
-            SDNR_HIP(hipMemsetAsync(changed, 0, sizeof(int), ctx->stream));
-            hipLaunchKernelGGL(apsp_relax_kernel, dim3((V + 255) / 256, (V + kRelaxRows - 1) / kRelaxRows),
-                               dim3(256), (size_t)Vp * 2, ctx->stream, V, Vp, ctx->max_indeg,
-                               ctx->radj16, kRelaxRows, D, changed);
-            SDNR_HIP(hipGetLastError());
-            int c = 1;
-            if ((rc = sdnr_fetch_ints(ctx, changed, 1, &c))) return rc;
-            if (!c) break;
-        }
     }
     return SDNR_OK;
 }

@@ -510,13 +510,11 @@ def test_shortest_global_path_torus(ctx):
     np.testing.assert_array_equal(nhp, nhpo)
 
 
-@pytest.mark.parametrize("algo", ["squaring", "squaring-norelax", "sq128", "fw"])
+@pytest.mark.parametrize("algo", ["squaring", "sq128", "fw"])
 @pytest.mark.parametrize("name", ["mock", "fat_tree_k8", "dragonfly_a4_h2_p2",
                                   "random_V60_dense", "torus_5x3x2", "random_V40", "random_V9"])
 def test_apsp_small(ctx, monkeypatch, name, algo):
-    if algo == "squaring-norelax":               # no one-edge relaxation check
-        monkeypatch.setenv("SDNROUTE_APSP_RELAX", "0")
-    elif algo != "squaring":
+    if algo != "squaring":
         monkeypatch.setenv("SDNROUTE_APSP", algo)
     csr = G.Golden(name).fabric().csr()
     ctx.upload(csr)
@@ -555,30 +553,23 @@ def test_shortest_unknown_destination_rows_device(ctx):
     assert (nh.cpu().numpy()[[0, 2]] == -1).all()
 
 
-@pytest.mark.parametrize("tiles", ["64", "sq128", "64-norelax"])
+@pytest.mark.parametrize("tiles", ["64", "sq128"])
 def test_apsp_fullsize_k48(ctx, monkeypatch, tiles):
-    """k=48 (diameter 4): with the one-edge relaxation check, 2 squarings
-    (the check after the second shows D exact); without it, 3."""
     if tiles == "sq128":
         monkeypatch.setenv("SDNROUTE_APSP", "sq128")
-    if tiles == "64-norelax":
-        monkeypatch.setenv("SDNROUTE_APSP_RELAX", "0")
     csr = T.fat_tree(48).csr()
     ctx.upload(csr)
     D = ctx.apsp()
     assert ctx.last_kernel() == ("minplus_square_kernel" if tiles == "sq128"
                                  else "minplus_square64_kernel")
-    assert ctx.last_launches() == (3 if tiles == "64-norelax" else 2)
     np.testing.assert_array_equal(D, O.apsp(csr))
 
 
-@pytest.mark.parametrize("tiles", ["64", "sq128", "64-norelax"])
+@pytest.mark.parametrize("tiles", ["64", "sq128"])
 def test_apsp_long_paths_torus(ctx, monkeypatch, tiles):
     """A high-diameter graph (ring-like torus 40x3x1): many squarings."""
     if tiles == "sq128":
         monkeypatch.setenv("SDNROUTE_APSP", "sq128")
-    if tiles == "64-norelax":
-        monkeypatch.setenv("SDNROUTE_APSP_RELAX", "0")
     csr = T.torus3d(40, 3, 1).csr()
     ctx.upload(csr)
     np.testing.assert_array_equal(ctx.apsp(), O.apsp(csr))
