@@ -619,9 +619,17 @@ typedef int (*shard_launch_fn)(sdnr_ctx *c, const int32_t *ids, int32_t n, void 
 // the shards of a multi-device context must not wait for each other there.
 // The first failing shard's error (rc + its thread's message) is returned.
 extern "C++" template <typename Fn>
-static int on_shard_threads(int n, Fn fn)
+static int on_shard_threads(int n, Fn fn, bool threaded)
 {
     if (n == 1) return fn(0);
+    if (!threaded) {
+        // launches that only enqueue (the DFS kernels) are issued in turn
+        // from this thread: a thread start + join per shard costs more than
+        // the launches themselves on small calls
+        for (int k = 0; k < n; ++k)
+            if (int rc = fn(k)) return rc;
+        return SDNR_OK;
+    }
     std::vector<int> rcs((size_t)n, SDNR_OK);
     std::vector<std::string> msgs((size_t)n);
     std::vector<std::thread> th;
@@ -637,6 +645,8 @@ static int on_shard_threads(int n, Fn fn)
         if (rcs[(size_t)k]) return sdnr_fail(rcs[(size_t)k], "%s", msgs[(size_t)k].c_str());
     return SDNR_OK;
 }
+
+static int shard_shortest(sdnr_ctx *c, const int32_t *ids, int32_t n, void *const o[3]);
 
 static int run_sharded(sdnr_ctx *ctx, const int32_t *ids, int32_t n, void *const out[3],
                        const size_t es[3], uint32_t flags, shard_launch_fn launch)
@@ -682,7 +692,7 @@ static int run_sharded(sdnr_ctx *ctx, const int32_t *ids, int32_t n, void *const
                                                 (size_t)cnt * V * es[i], c->stream));
             SDNR_HIP(hipEventRecord(c->ev_join, c->stream));
             return SDNR_OK;
-        });
+        }, launch == shard_shortest);   // the plane BFS polls the host between levels
         ctx->timed = timed;
         SDNR_HIP(hipSetDevice(ctx->device));
         if (rc) return rc;
@@ -718,7 +728,7 @@ static int run_sharded(sdnr_ctx *ctx, const int32_t *ids, int32_t n, void *const
                                         d_outs[k][i], (size_t)cnt * V * es[i],
                                         hipMemcpyDeviceToHost, c->stream));
         return SDNR_OK;
-    });
+    }, true);      // pageable host copies block: one thread per shard
     int first = rc;
     for (int k = 0; k < nctx; ++k) {
         sdnr_ctx *c = sub(k);

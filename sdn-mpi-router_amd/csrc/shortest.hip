@@ -873,7 +873,10 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
     // pad (tools/bimodal_settings.py).  SDNROUTE_PLANE_PAD
     // overrides the pad (words).
     int VS = V + 64;
-    if (const char *f = getenv("SDNROUTE_PLANE_PAD")) VS = V + atoi(f);
+    if (const char *f = getenv("SDNROUTE_PLANE_PAD")) {     // words; a stride below V would
+        const int pad = atoi(f);                              // overlap the planes
+        if (pad >= 0 && pad <= (1 << 16)) VS = V + pad;
+    }
     const size_t per_batch = (size_t)plane_count(sb) * VS * sizeof(uint64_t);
     // batches per chunk: the planes one level sweeps stay inside the 256 MiB
     // Infinity Cache (measured: torus 32^3 14.9 -> 12.8 ms with 64 batches of

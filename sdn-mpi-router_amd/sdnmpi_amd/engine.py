@@ -192,6 +192,33 @@ def _where(c, a, b):
     return b.masked_fill(c, a)
 
 
+def _edge_keys_host(csr):
+    """(keys int64 ascending = x * V + col of every CSR entry, port int32)."""
+    rp = np.asarray(csr.row_ptr, np.int64)
+    keys = np.repeat(np.arange(csr.V, dtype=np.int64), np.diff(rp)) * csr.V + \
+        np.asarray(csr.col, np.int64)
+    return keys, np.asarray(csr.port, np.int32)
+
+
+def _next_hop_port(nh, keys, port, V):
+    """CSR port of edge (x, nh[r, x]) for every entry of an int64 next-hop
+    block (-1 where nh < 0); numpy or device tensors."""
+    if keys.shape[0] == 0:
+        return nh * 0 - 1
+    n = nh.shape[-1]
+    if _is_np(nh):
+        x = np.broadcast_to(np.arange(n, dtype=np.int64), nh.shape)
+        ok = nh >= 0
+        e = np.minimum(np.searchsorted(keys, np.where(ok, x * V + nh, 0)), keys.shape[0] - 1)
+        return np.where(ok, port[e].astype(np.int64), -1)
+    t = _torch()
+    x = t.arange(n, dtype=t.int64, device=nh.device).expand_as(nh)
+    ok = nh >= 0
+    k = (x * V + nh).masked_fill(~ok, 0)
+    e = t.searchsorted(keys, k).clamp_(max=keys.shape[0] - 1)
+    return port[e].to(t.int64).masked_fill(~ok, -1)
+
+
 def pack_host_tree(parent, port, csr, layout):
     """Host (numpy) tables -> tree words (int32 storage): the test double's
     counterpart of sdnr_tree_pack."""
@@ -225,6 +252,7 @@ class RouteEngine(object):
         self.dev = torch.device("cuda", self.devices[0])
         self._loaded = None
         self._csr_dev = None        # (export, row_ptr int64, port int32) on the device
+        self._keys_dev = None       # (export, edge keys int64, port int32) on the device
 
     # -- plumbing -------------------------------------------------------
     def _ready(self):
@@ -252,6 +280,16 @@ class RouteEngine(object):
             self._csr_dev = (export, t.from_numpy(np.asarray(c.row_ptr, np.int64)).to(self.dev),
                              t.from_numpy(np.asarray(c.port, np.int32)).to(self.dev))
         return self._csr_dev[1], self._csr_dev[2]
+
+    def edge_keys_device(self, export):
+        """(keys int64 = x * V + col per CSR entry, ascending; port int32) on
+        the device: the next-hop port lookups of the shortest tables."""
+        if self._keys_dev is None or self._keys_dev[0] is not export:
+            keys, port = _edge_keys_host(export.csr)
+            t = self._torch
+            self._keys_dev = (export, t.from_numpy(keys).to(self.dev),
+                              t.from_numpy(port).to(self.dev))
+        return self._keys_dev[1], self._keys_dev[2]
 
     # -- tables (device-resident) ---------------------------------------
     def dfs_tables(self, export, srcs, with_hops=True):
@@ -593,12 +631,22 @@ class TableCache(object):
             return None, None
         return Wide(a[0], "u16raw"), Wide(a[1], "u16" if self.V <= 0xFFFF else "int")
 
-    def sp_host(self, slots):
-        """(dist u16, nh int64) numpy rows of pool slots."""
+    def sp_decoded(self, slots, engine=None):
+        """(dist u16, nh int32, nh_port int32) numpy rows of pool slots.  The
+        next hop's port -- ``links[x][nh].src.port_no``, the CSR port of edge
+        (x, nh) -- is looked up where the rows live (on the device for a
+        device pool), so only the three output planes cross to the host."""
         a = self.sp.tables()
-        d = _host(_take(a[0], slots)).view(np.uint16)
-        nh = _host(_take(a[1], slots))
-        return d, (_u16(nh) if self.V <= 0xFFFF else nh.astype(np.int64))
+        d = _take(a[0], slots)
+        nh = _take(a[1], slots)
+        nh = _u16(nh) if self.V <= 0xFFFF else _i64(nh)
+        if _is_np(nh):
+            keys, port = _edge_keys_host(self.export.csr)
+        else:
+            keys, port = engine.edge_keys_device(self.export)
+        nhp = _next_hop_port(nh, keys, port, self.V)
+        return (_host(d).view(np.uint16), _host(nh).astype(np.int32),
+                _host(nhp).astype(np.int32))
 
     # -- graph changes ---------------------------------------------------
     def retarget(self, export, diff):
@@ -615,6 +663,8 @@ class TableCache(object):
             verts = self.dfs.slot_vertices()
             hit = np.asarray(dfs_rows_affected(par, hop, verts, diff), bool) & (verts >= 0)
             self.dfs.drop(verts[hit].tolist())
+            if self.layout == SLOT:
+                self._reslot(diff)
             self.rows_inherited += len(self.dfs.row)
         if self.sp.row:
             dist, nh = self.sp_views()
@@ -625,6 +675,71 @@ class TableCache(object):
         self.dfs.host.clear()
         self.sp.host.clear()
         return True
+
+    RESLOT_ROWS = 256             # pool rows per re-slot pass (bounded temporaries)
+
+    def _reslot(self, diff):
+        """Slot trees name a position in the parent's CSR row, and a link
+        added to or removed from row u moves the later positions of row u.
+        The rows kept across the change are still the right trees (the row
+        tests above are about the tree, not the encoding), so every kept
+        entry whose parent's row changed gets its slot re-derived from the
+        new CSR: the position of (parent, v) in the new row of the parent.
+        The edge exists: a kept tree's edges are unaffected by the change."""
+        rows_changed = np.unique(np.concatenate([diff.removed[0], diff.added[0]]))
+        a = self.dfs.tables()
+        if a is None or rows_changed.size == 0 or not self.dfs.row:
+            return
+        csr = self.export.csr
+        V = csr.V
+        rp = np.asarray(csr.row_ptr, np.int64)
+        # keys (p * V + v) -> global edge index, for the changed rows only
+        lo, hi = rp[rows_changed], rp[rows_changed + 1]
+        eidx = np.concatenate([np.arange(s, e, dtype=np.int64) for s, e in zip(lo, hi)]) \
+            if rows_changed.size else np.zeros(0, np.int64)
+        src = np.repeat(rows_changed.astype(np.int64), hi - lo)
+        keys = src * V + np.asarray(csr.col, np.int64)[eidx]     # ascending: rows sorted
+        changed = np.zeros(V, bool)
+        changed[rows_changed] = True
+        tree = a[0]
+        used = np.sort(np.fromiter(self.dfs.row.values(), np.int64, len(self.dfs.row)))
+        if _is_np(tree):
+            xp_keys, xp_e, xp_rp, xp_ch = keys, eidx, rp, changed
+        else:
+            t = _torch()
+            dv = tree.device
+            xp_keys = t.from_numpy(keys).to(dv)
+            xp_e = t.from_numpy(eidx).to(dv)
+            xp_rp = t.from_numpy(rp).to(dv)
+            xp_ch = t.from_numpy(changed).to(dv)
+        for i in range(0, used.size, self.RESLOT_ROWS):
+            sl = used[i:i + self.RESLOT_ROWS]
+            w = _take(tree, sl)
+            x = _i64(w) & 0xFFFFFFFF
+            par = x & 0x3FFFFFF
+            slot = x >> 26
+            need = (x != 0xFFFFFFFF) & (slot != 63)
+            if _is_np(x):
+                need &= xp_ch[np.where(need, par, 0)]
+                if not need.any():
+                    continue
+                r, v = np.nonzero(need)
+                p = par[r, v]
+                e = np.searchsorted(xp_keys, p * V + v)
+                assert np.all(xp_keys[e] == p * V + v), "kept tree edge missing"
+                x[r, v] = p | ((xp_e[e] - xp_rp[p]) << 26)
+                tree[sl] = (x & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
+            else:
+                need &= xp_ch[par.masked_fill(~need, 0)]
+                if not bool(need.any()):
+                    continue
+                r, v = t.nonzero(need, as_tuple=True)
+                p = par[r, v]
+                k = p * V + v
+                e = t.searchsorted(xp_keys, k)
+                x[r, v] = p | ((xp_e[e] - xp_rp[p]) << 26)
+                x = t.where(x >= (1 << 31), x - (1 << 32), x).to(t.int32)
+                tree.index_copy_(0, t.as_tensor(sl, device=dv), x)
 
     # -- filling ---------------------------------------------------------
     def _rows(self, store, compute, wanted, batch):

@@ -38,6 +38,7 @@ except Exception:   # noqa: BLE001 - Ryu is not a dependency of the engine
 __all__ = ["TopologyDB", "OFPP_LOCAL"]
 
 _INF = 0xFFFF
+TABLE_SLICE_ENTRIES = 1 << 24     # table entries decoded per slice by route_tables()
 
 
 class TopologyDB(object):
@@ -322,22 +323,30 @@ class TopologyDB(object):
         c = self._cache
         store = c.dfs if mode == "dfs" else c.sp
         get = c.dfs_rows if mode == "dfs" else c.sp_rows
-        parts = []                    # host copies, a budget's worth of rows at a time
+        V = ex.csr.V
+        n = len(hv)
+        cols = [np.empty((n, V), np.int32), np.empty((n, V), np.int32),
+                np.empty((n, V), np.int32)] if mode == "dfs" else \
+            [np.empty((n, V), np.uint16), np.empty((n, V), np.int32), np.empty((n, V), np.int32)]
         step = max(1, store.cap())
-        for i in range(0, len(hv), step):
+        # decoded a bounded slice at a time (int64 temporaries of a whole
+        # budget's rows would be tens of GB on the torus / Jellyfish)
+        sl = max(1, TABLE_SLICE_ENTRIES // max(1, V))
+        for i in range(0, n, step):                 # a budget's worth of rows at a time
             chunk = hv[i:i + step]
             get(self.engine, chunk)
             idx = np.asarray([store.row[v] for v in chunk], np.int64)
-            if mode == "dfs":
-                parts.append(tuple(_host(a).astype(np.int32) for a in c.dfs_int32(idx, self.engine)))
-            else:
-                d, nh = c.sp_host(idx)
-                parts.append((d, nh.astype(np.int32), _edge_ports(ex.csr, nh)))
-        V = ex.csr.V
-        empty = (np.zeros((0, V), np.int32), np.zeros((0, V), np.int32),
-                 np.zeros((0, V), np.int32)) if mode == "dfs" else \
-            (np.zeros((0, V), np.uint16), np.zeros((0, V), np.int32), np.zeros((0, V), np.int32))
-        cols = [np.concatenate([p[k] for p in parts]) if parts else empty[k] for k in range(3)]
+            for j in range(0, len(chunk), sl):
+                part = idx[j:j + sl]
+                r0, r1 = i + j, i + j + part.size
+                if mode == "dfs":
+                    for k, a in enumerate(c.dfs_int32(part, self.engine)):
+                        cols[k][r0:r1] = _host(a)
+                else:
+                    d, nh, nhp = c.sp_decoded(part, self.engine)
+                    cols[0][r0:r1] = d
+                    cols[1][r0:r1] = nh
+                    cols[2][r0:r1] = nhp
         if mode == "dfs":
             return {"sources": np.asarray(hv, np.int32), "parent": cols[0],
                     "port": cols[1], "hops": cols[2], "dpids": ex.csr.dpids}
@@ -461,22 +470,6 @@ class TopologyDB(object):
             if len(want) < self._cache.dfs.cap():
                 self._cache.dfs_rows(self.engine, sorted(want), self._host_vertices(ex))
         return [self.find_route(a, b, multiple) for a, b in pairs]
-
-
-def _edge_ports(csr, nh):
-    """links[x][nh[r, x]].src.port_no for every entry (-1 where nh < 0): the
-    next hops' ports, looked up in the CSR."""
-    V = csr.V
-    rp = np.asarray(csr.row_ptr, np.int64)
-    keys = np.repeat(np.arange(V, dtype=np.int64), np.diff(rp)) * V + \
-        np.asarray(csr.col, np.int64)
-    x = np.broadcast_to(np.arange(V, dtype=np.int64), nh.shape)
-    ok = nh >= 0
-    e = np.searchsorted(keys, np.where(ok, x * V + nh, 0))
-    e = np.minimum(e, max(keys.shape[0] - 1, 0))
-    if keys.shape[0] == 0:
-        return np.full(nh.shape, -1, np.int32)
-    return np.where(ok, np.asarray(csr.port, np.int32)[e], -1).astype(np.int32)
 
 
 def _same_graph(a, b):

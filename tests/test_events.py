@@ -197,3 +197,53 @@ def test_jellyfish_events_are_o_change():
     print("host-code ms: add_host+find_route %.1f, delete_link+find_route %.1f" % (ms_host, ms_link))
     assert ms_host <= 50.0, ms_host
     assert ms_link <= 50.0, ms_link
+
+
+def _slot_event_replay(kind, fake):
+    """Slot trees (``parent | slot << 26``, the layout of fabrics with a port
+    >= 0xFFFF or more than 65,535 switches) name a position in the parent's
+    CSR row; a link added to or removed from that row moves the later
+    positions.  Rows the cache keeps across such an event must still decode
+    to the right ports (246 wrong routes before the fix)."""
+    from sdnmpi_amd.engine import SLOT
+    rng = np.random.default_rng({"delete": 3, "add": 4, "mixed": 5}[kind])
+    fabric = T.fat_tree(4)
+    db = fabric.populate(TopologyDB())
+    if fake:
+        db._engine = _FakeEngine()
+    u0 = sorted(db.links)[0]
+    v0 = sorted(db.links[u0])[0]
+    lk = db.links[u0][v0]
+    db.links[u0][v0] = Link(Port(u0, 70000), Port(v0, lk.dst.port_no))
+    macs = sorted(db.hosts)
+    pairs = [(a, b) for a in macs for b in macs]
+    for a, b in pairs:                        # fill the cache with every row
+        db.find_route(a, b)
+    assert db._cache.layout == SLOT
+    dpids = sorted(db.switches)
+    for step in range(30):
+        links = [(u, v) for u, nb in db.links.items() for v in nb]
+        if kind == "delete" or (kind == "mixed" and step % 2 == 0):
+            u, v = links[int(rng.integers(len(links)))]
+            db.delete_link(db.links[u][v])
+        else:
+            u, v = (int(x) for x in rng.choice(dpids, 2, replace=False))
+            if v in db.links.get(u, {}):
+                continue
+            db.add_link(Link(Port(u, int(rng.integers(40, 60))), Port(v, 9)))
+        for a, b in pairs[int(rng.integers(0, 7))::7]:
+            assert db.find_route(a, b) == O.find_route_pair(db, a, b), (kind, step)
+    assert db._cache.rows_inherited > 0
+
+
+@pytest.mark.parametrize("kind", ["delete", "add", "mixed"])
+def test_slot_layout_keeps_rows_across_link_events(kind):
+    _slot_event_replay(kind, fake=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["delete", "add", "mixed"])
+def test_slot_layout_keeps_rows_across_link_events_gpu(kind):
+    """The same replay on the device pool (the re-slot runs as torch ops
+    where the rows live)."""
+    _slot_event_replay(kind, fake=False)
