@@ -53,7 +53,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--fabric", default="fat_tree:48")
-    ap.add_argument("--mode", choices=["dfs", "shortest", "flows", "ecmp", "apsp"], default="dfs")
+    ap.add_argument("--mode", choices=["dfs", "shortest", "flows", "ecmp", "apsp", "matflows"],
+                    default="dfs")
     ap.add_argument("--ranks", type=int, default=1024,
                     help="flows mode: MPI ranks placed on random hosts; every ordered "
                          "rank pair's flow entries are emitted per step")
@@ -132,22 +133,29 @@ def cpu_baseline(fabric, csr, srcs, hosts_per_src, H, budget_s):
            "sample": "oracle/sdnroute_oracle.c per-source DFS trees (same algorithm, "
                      "pthreads, %d threads) for %d of %d sources x %d repetitions, %.2f s"
                      % (threads, n, len(srcs), reps, dt)}
-    # the reference's own shape: one Python stack search per host pair
+    # the reference's own shape: one Python stack search per host pair, with
+    # the reference's path copies (topology_db.py:59-84), and beside it the
+    # same search keeping predecessor links (a faster restatement)
     db = _DictDB()
     fabric.populate(db)
     macs = fabric.host_macs()
-    rng = np.random.default_rng(0)
-    t0 = time.perf_counter()
-    k = 0
-    while time.perf_counter() - t0 < min(5.0, budget_s / 4):
-        a, b = rng.integers(0, len(macs), 2)
-        O.find_route_pair(db, macs[a], macs[b])
-        k += 1
-    dt = time.perf_counter() - t0
-    ref = {"value": k / dt, "unit": "routes/s", "cores": 1, "kind": "port",
-           "sample": "oracle.find_route_pair (per-pair Python LIFO search, the "
-                     "reference's algorithm shape) on %d random host pairs, %.2f s" % (k, dt)}
-    return out, ref
+    res = []
+    for copying in (True, False):
+        rng = np.random.default_rng(0)
+        t0 = time.perf_counter()
+        k = 0
+        while time.perf_counter() - t0 < min(5.0, budget_s / 4):
+            a, b = rng.integers(0, len(macs), 2)
+            O.find_route_pair(db, macs[a], macs[b], copying=copying)
+            k += 1
+        dt = time.perf_counter() - t0
+        res.append({"value": k / dt, "unit": "routes/s", "cores": 1, "kind": "port",
+                    "sample": "oracle.find_route_pair(copying=%s): per-pair Python LIFO search "
+                              "%s on %d random host pairs, %.2f s" % (
+                                  copying, "copying the path list on every push, as "
+                                  "topology_db.py:79 does" if copying else
+                                  "keeping predecessor links (not the reference's cost)", k, dt)})
+    return out, res[0], res[1]
 
 
 _MP_DB = None
@@ -164,7 +172,7 @@ def _mp_pairs(args):
     k = 0
     while time.perf_counter() - t0 < secs:
         a, b = rng.integers(0, len(macs), 2)
-        O.find_route_pair(db, macs[a], macs[b])
+        O.find_route_pair(db, macs[a], macs[b], copying=True)
         k += 1
     return k, time.perf_counter() - t0
 
@@ -184,8 +192,9 @@ def cpu_reference_path_mp(fabric, secs=5.0):
     _MP_DB = None
     rate = sum(k / dt for k, dt in res)
     return {"value": rate, "unit": "routes/s", "cores": procs, "kind": "port",
-            "sample": "oracle.find_route_pair in %d forked processes, %d random host pairs "
-                      "in %.1f s each" % (procs, sum(k for k, _ in res), secs)}
+            "sample": "oracle.find_route_pair(copying=True) (the reference's path-copying "
+                      "search) in %d forked processes, %d random host pairs in %.1f s each" % (
+                          procs, sum(k for k, _ in res), secs)}
 
 
 class _DictDB(object):
@@ -200,6 +209,68 @@ class _DictDB(object):
 
     def add_host(self, h):
         self.hosts[h.mac] = h
+
+
+def dropin_block(fabric, queries=10000, seed=5):
+    """The drop-in as the controller calls it (reference sdnmpi/topology.py:
+    138-142: one find_route per packet-in; :184-202: link events), timed on
+    the host clock: TopologyDB (sdnmpi_amd.util.topology_db) over this GPU.
+
+    cold_ms        first find_route: CSR export + upload + the trees of every
+                   host-bearing switch into the device pool + one row to host;
+    warm_us        mean per find_route over `queries` random host pairs
+                   (one tree row copied to host per source miss, host LRU);
+    batched_us     the same pairs through find_routes (route_entries: one
+                   device expansion for all of them), per pair;
+    event_ms       delete_link of a link on a cached route + the requery (the
+                   rows the link can change recomputed), then add_link back
+                   + requery."""
+    from sdnmpi_amd.util.topology_db import TopologyDB
+    db = fabric.populate(TopologyDB())
+    macs = fabric.host_macs()
+    rng = np.random.default_rng(seed)
+    pairs = [(macs[int(a)], macs[int(b)]) for a, b in rng.integers(0, len(macs), (queries, 2))]
+    t0 = time.perf_counter()
+    route = db.find_route(*pairs[0])
+    cold = (time.perf_counter() - t0) * 1e3
+    kernel = db.engine.ctx.last_kernel()
+    rows = len(db._cache.dfs)
+    t0 = time.perf_counter()
+    for a, b in pairs:
+        db.find_route(a, b)
+    warm = (time.perf_counter() - t0) / len(pairs) * 1e6
+    t0 = time.perf_counter()
+    batch = db.find_routes(pairs)
+    batched = (time.perf_counter() - t0) / len(pairs) * 1e6
+    assert batch[0] == route
+    i = next(k for k in range(len(pairs)) if len(batch[k]) >= 3)   # a multi-switch route
+    route = batch[i]
+    pairs[0] = pairs[i]
+    u, v = route[1][0], None
+    for w, lk in db.links[u].items():
+        if lk.src.port_no == route[1][1]:
+            v = w
+    link = db.links[u][v]
+    t0 = time.perf_counter()
+    db.delete_link(link)
+    db.find_route(*pairs[0])
+    t_del = (time.perf_counter() - t0) * 1e3
+    recomputed = db._cache.rows_computed
+    t0 = time.perf_counter()
+    db.add_link(link)
+    back = db.find_route(*pairs[0])
+    t_add = (time.perf_counter() - t0) * 1e3
+    assert back == route
+    out = {"cold_ms": cold, "cold_rows": rows, "kernel": kernel, "warm_us": warm,
+           "batched_us": batched, "queries": len(pairs),
+           "delete_link_requery_ms": t_del, "add_link_requery_ms": t_add,
+           "rows_computed_total": recomputed,
+           "note": "TopologyDB.find_route as the controller calls it (host clock): cold = "
+                   "first query (export, upload, all host-switch trees into the device "
+                   "pool); warm = mean per query over random host pairs; batched = "
+                   "find_routes over the same pairs; link event + requery"}
+    db.engine.close()
+    return out
 
 
 def materialised_flows(ctx, dev, stream, csr, fabric, srcs, chunk=1 << 24):
@@ -264,6 +335,30 @@ def materialised_flows(ctx, dev, stream, csr, fabric, srcs, chunk=1 << 24):
                     "(offsets + route_jump expansion per %d-pair chunk, one reused output "
                     "buffer), tables and requests resident; compare the headline, which "
                     "counts pairs whose route the tables determine" % (H, chunk)}
+
+
+def main_matflows(args, world, rank, local, dev):
+    """The default line's materialised_flows block alone (profiling): every
+    host pair's fdb written to HBM, --steps repetitions."""
+    fabric = T.by_name(args.fabric)
+    csr = fabric.csr()
+    hv, _ = fabric.host_table()
+    srcs = np.unique(hv).astype(np.int32)
+    ctx = _native.Context(local)
+    ctx.upload(csr)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    res = [materialised_flows(ctx, dev, stream, csr, fabric, srcs)
+           for _ in range(max(1, args.steps))]
+    best = min(res, key=lambda r: r["ms"])
+    if rank == 0:
+        print(json.dumps({"metric": "materialised flow entries of all host pairs, pairs/sec",
+                          "value": best["value"], "unit": "routes/s", "n_gpus": 1,
+                          "ms_per_step": best["ms"], "all_ms": [r["ms"] for r in res],
+                          "steps": len(res), "higher_is_better": True,
+                          "config": {"workload": "%s materialised flows" % args.fabric},
+                          "materialised_flows": best}), flush=True)
+    ctx.close()
 
 
 def main_flows(args, world, rank, local, dev):
@@ -471,11 +566,13 @@ def main_apsp(args, world, rank, local, dev):
     ms = (time.perf_counter() - t0) / args.steps * 1e3
     kern_ms = float(np.mean(kms))
     passes = ctx.last_launches()            # squaring passes of one APSP call
-    # algorithmic: one add + one min per (i, j, k) per pass over the V x V
-    # matrix (the kernels pad V to their tile: 64, or 128 for sq128)
-    tile = 64 if ctx.last_kernel() == "minplus_square64_kernel" else 128
+    sweeps = ctx.last_sweeps()              # Bellman-Ford sweeps (apsp_relax8_kernel)
+    # algorithmic: one add + one min per (i, j, k) per squaring pass over the
+    # V x V matrix (the kernels pad V to their tile: 64, or 128 for sq128),
+    # and per (i, edge k -> j) per sweep
+    tile = 128 if ctx.last_kernel() == "minplus_square_kernel" else 64
     Vp = (V + tile - 1) // tile * tile
-    ops = passes * 2.0 * float(V) ** 3
+    ops = passes * 2.0 * float(V) ** 3 + sweeps * 2.0 * float(V) * csr.E
     achieved = ops / (kern_ms / 1e3) / 1e12
     # VALU peak: 256 CUs x 4 SIMDs x 32 lanes x 2 (packed u16) ops/clk x 2.4 GHz
     peak = 256 * 4 * 32 * 2 * 2.4e9 / 1e12
@@ -490,6 +587,7 @@ def main_apsp(args, world, rank, local, dev):
                      "frac": achieved / peak, "traffic": _traffic("%s/apsp/N1" % args.fabric),
                      "kernel": ctx.last_kernel(),
                      "kernel_ms": kern_ms, "ops_per_launch": ops, "passes": passes,
+                     "sweeps": sweeps,
                      "padded_ops_per_launch": passes * 2.0 * float(Vp) ** 3,
                      **_measured(_traffic("%s/apsp/N1" % args.fabric), kern_ms)},
     }
@@ -626,6 +724,8 @@ def main():
         return main_ecmp(args, world, rank, local, dev)
     if args.mode == "apsp":
         return main_apsp(args, world, rank, local, dev)
+    if args.mode == "matflows":
+        return main_matflows(args, world, rank, local, dev)
 
     fabric = T.by_name(args.fabric)
     csr = fabric.csr()
@@ -821,10 +921,16 @@ def main():
     if rank == 0 and world == 1 and args.mode == "dfs" and not args.max_sources and \
             not args.no_flows and args.fabric.startswith("fat_tree"):
         out["materialised_flows"] = materialised_flows(ctx, dev, stream, csr, fabric, srcs)
+    if rank == 0 and world == 1 and args.mode == "dfs" and not args.max_sources and \
+            not args.no_flows and args.fabric.startswith("fat_tree"):
+        out["dropin"] = dropin_block(fabric)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "dfs":
-        base, ref = cpu_baseline(fabric, csr, srcs, counts, H, args.cpu_budget_s)
+        base, ref, ref_pred = cpu_baseline(fabric, csr, srcs, counts, H, args.cpu_budget_s)
+        if "dropin" in out:   # the reference's own cost per query, beside the drop-in's
+            out["dropin"]["cpu_reference_ms_per_route"] = 1e3 / ref["value"]
         out["cpu_baseline"] = base
         out["cpu_reference_path"] = ref
+        out["cpu_reference_path_pred"] = ref_pred
         if ref_mp is not None:
             out["cpu_reference_path_all_cores"] = ref_mp
         out["gpu_over_cpu"] = value / base["value"]

@@ -153,6 +153,19 @@ int sdnr_dfs_tables_slots(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc,
 int sdnr_tree_pack(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port,
                    int64_t n, uint32_t *tree, int32_t layout, uint32_t flags);
 
+/* Default-route trees straight in a 4-byte layout (SDNR_TREE_PORT16 as
+ * sdnr_dfs_tables_packed, SDNR_TREE_SLOT as sdnr_dfs_tables_slots) plus the
+ * tree depth -- the rows the Python TopologyDB's route cache keeps (the
+ * route lengths of _route_to_fdb, topology_db.py:127-138, and the
+ * incremental row tests need the depth):
+ *   depth[i*V+v]  hops src[i] -> v; depth_bytes 2: u16, 0xFFFF unreachable
+ *                 (needs V <= 65535), 4: int32, -1 unreachable; NULL: none.
+ * The same kernels as the benched packed / slot tables, with no int32
+ * intermediate. */
+int sdnr_dfs_tables_tree(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc,
+                         uint32_t *tree, void *depth, int32_t layout,
+                         int32_t depth_bytes, uint32_t flags);
+
 /* Shortest routes, find_route(src, dst, multiple=True) -> _find_routes_bfs
  * (topology_db.py:86-122, called from :168-180), as per-destination tables:
  * for every destination dst[i] and every vertex x
@@ -232,6 +245,10 @@ int sdnr_last_kernel_ms(sdnr_ctx *ctx, float *ms);
  * min-plus squaring passes of sdnr_apsp, the BFS levels of the level-by-level
  * shortest kernel, 1 for single-launch kernels (0 before the first call). */
 int sdnr_last_launches(const sdnr_ctx *ctx, int32_t *launches);
+
+/* Bellman-Ford sweeps of the last sdnr_apsp call (the most any 8-row block
+ * ran, summed over its relaxation launches; 0 with SDNROUTE_APSP_RELAX=0). */
+int sdnr_last_sweeps(const sdnr_ctx *ctx, int32_t *sweeps);
 
 /* Name of the kernel variant the last table call launched on this context
  * (e.g. "dfs_count_kernel<4>"; "" before the first call). */

@@ -183,13 +183,38 @@ def _dfs_path(links, s, d):
     return []
 
 
-def find_route_pair(db, src_mac, dst_mac):
-    """find_route(src_mac, dst_mac) (multiple=False), reference semantics."""
+def _dfs_path_copying(links, s, d):
+    """The stack search of topology_db.py:59-84 in the reference's own shape:
+    a visited set (:63), a stack of whole paths (:65), and a fresh copy of the
+    popped path for every pushed neighbour (:79-82) -- the per-pair cost the
+    controller pays per packet-in.  Same result as _dfs_path."""
+    visited = set([s])
+    paths = [[s]]
+    while paths:
+        current = paths.pop()
+        u = current[-1]
+        if u == d:
+            return current
+        if u not in links:
+            continue
+        for v in sorted(links[u].keys()):
+            if v not in visited:
+                nxt = list(current)
+                nxt.append(v)
+                visited.add(v)
+                paths.append(nxt)
+    return []
+
+
+def find_route_pair(db, src_mac, dst_mac, copying=False):
+    """find_route(src_mac, dst_mac) (multiple=False), reference semantics.
+    ``copying``: search with the reference's path copies (_dfs_path_copying,
+    the reference's cost) instead of predecessor links (_dfs_path)."""
     ep = _endpoints(db, src_mac, dst_mac)
     if ep is None:
         return []
     s, d, d_local = ep
-    seq = _dfs_path(db.links, s, d)
+    seq = (_dfs_path_copying if copying else _dfs_path)(db.links, s, d)
     if not seq:
         return []
     return _to_fdb(db, seq, d, d_local, dst_mac)

@@ -366,6 +366,113 @@ __global__ __launch_bounds__(128) void minplus_square64_kernel(int Vp, uint16_t 
     if (lane_id() == 0) atomicMax(reinterpret_cast<unsigned *>(changed) + 1, mx);
 }
 
+// Bellman-Ford sweeps, 8 rows at a time: row i of D holds upper bounds of
+// the hop distances from i (every entry is the length of a real path), and
+// D[i][j] <- min(D[i][j], min over in-neighbours k of j of D[i][k] + 1)
+// keeps that true while extending the exact horizon by at least one hop per
+// sweep; a sweep that changes nothing proves the row exact (D[i][i] = 0 and
+// the edge inequalities hold everywhere: by induction on path length).  The
+// rows of one source depend on nothing else, so a block iterates its 8 rows
+// to that fixpoint (or `cap` sweeps) in LDS with no grid-wide step, and
+// writes them back.  Rows staged TRANSPOSED (column j -> its 8 row values,
+// one 16-byte entry): one ds_read_b128 per in-neighbour k serves all 8
+// rows, the relaxation is 4 v_pk_add_u16 (clamp) + 4 v_pk_min_u16; sweeps
+// update in place (any interleaving keeps valid upper bounds).  Small-
+// diameter sparse fabrics (k=48: diameter 4) converge here in a handful of
+// V^2 x in-degree sweeps, where each squaring pass costs V^3.
+// changed[0]: some block did not reach its fixpoint within cap sweeps;
+// changed[1]: the most sweeps any block ran.
+__global__ __launch_bounds__(1024) void apsp_relax8_kernel(int V, int Vp, int maxd,
+                                                          const uint16_t *__restrict__ radj,
+                                                          uint16_t *__restrict__ D,
+                                                          int *__restrict__ changed, int cap)
+{
+    extern __shared__ uint4 L[];                 // L[j] = D[i0..i0+7][j] as 8 u16
+    const int i0 = blockIdx.x * 8;
+    for (int j = threadIdx.x; j < V; j += blockDim.x) {
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int ra = i0 + 2 * q, rb = ra + 1;
+            const uint32_t a = ra < V ? D[(size_t)ra * Vp + j] : 0xFFFFu;
+            const uint32_t b = rb < V ? D[(size_t)rb * Vp + j] : 0xFFFFu;
+            w[q] = a | (b << 16);
+        }
+        L[j] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    __syncthreads();
+    const u16x2 one = {1, 1};
+    bool any = false, ch = true;
+    int sweeps = 0;
+    while (ch && sweeps < cap) {
+        ch = false;
+        ++sweeps;
+        for (int j = threadIdx.x; j < V; j += blockDim.x) {
+            const uint32_t *rr = reinterpret_cast<const uint32_t *>(radj + (size_t)j * 64);
+            uint32_t nb[32];                     // in-row of j, sentinel V
+#pragma unroll
+            for (int q = 0; q < 32; ++q) nb[q] = rr[q];
+            const uint4 c = L[j];
+            u16x2 cur[4], best[4];
+            cur[0] = __builtin_bit_cast(u16x2, c.x);
+            cur[1] = __builtin_bit_cast(u16x2, c.y);
+            cur[2] = __builtin_bit_cast(u16x2, c.z);
+            cur[3] = __builtin_bit_cast(u16x2, c.w);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) best[r] = cur[r];
+#pragma unroll
+            for (int q = 0; q < 32; ++q) {
+                if (2 * q < maxd) {              // uniform: rows hold <= maxd entries
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const uint32_t k = h ? nb[q] >> 16 : nb[q] & 0xFFFFu;
+                        if (k < (uint32_t)V) {
+                            const uint4 x = L[k];
+                            best[0] = __builtin_elementwise_min(
+                                best[0], __builtin_elementwise_add_sat(__builtin_bit_cast(u16x2, x.x), one));
+                            best[1] = __builtin_elementwise_min(
+                                best[1], __builtin_elementwise_add_sat(__builtin_bit_cast(u16x2, x.y), one));
+                            best[2] = __builtin_elementwise_min(
+                                best[2], __builtin_elementwise_add_sat(__builtin_bit_cast(u16x2, x.z), one));
+                            best[3] = __builtin_elementwise_min(
+                                best[3], __builtin_elementwise_add_sat(__builtin_bit_cast(u16x2, x.w), one));
+                        }
+                    }
+                }
+            }
+            bool d = false;                      // INF + 1 saturates: never below INF
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                d |= __builtin_bit_cast(uint32_t, best[r]) != __builtin_bit_cast(uint32_t, cur[r]);
+            if (d) {
+                L[j] = make_uint4(__builtin_bit_cast(uint32_t, best[0]),
+                                  __builtin_bit_cast(uint32_t, best[1]),
+                                  __builtin_bit_cast(uint32_t, best[2]),
+                                  __builtin_bit_cast(uint32_t, best[3]));
+                ch = true;
+            }
+        }
+        ch = __syncthreads_or(ch);
+        any |= ch;
+    }
+    if (any) {                                   // write the improved rows back
+        for (int j = threadIdx.x; j < V; j += blockDim.x) {
+            const uint4 c = L[j];
+            const uint32_t w[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int ra = i0 + 2 * q, rb = ra + 1;
+                if (ra < V) D[(size_t)ra * Vp + j] = (uint16_t)(w[q] & 0xFFFFu);
+                if (rb < V) D[(size_t)rb * Vp + j] = (uint16_t)(w[q] >> 16);
+            }
+        }
+    }
+    if (threadIdx.x == 0) {
+        if (ch) atomicOr(changed, 1);            // cap reached before the fixpoint
+        atomicMax(changed + 1, sweeps);
+    }
+}
+
 }  // namespace
 
 static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp, int mt)
@@ -377,12 +484,40 @@ static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp, int m
                        ctx->row_ptr, ctx->col, D);
     hipLaunchKernelGGL(apsp_edges_kernel, dim3((V + 255) / 256), dim3(256), 0, ctx->stream, V, Vp,
                        ctx->row_ptr, ctx->col, D);
-    // stop when a pass changes nothing, or when after s squarings (exact for
-    // every distance <= 2^s) the largest finite distance M is < 2^s: no pair
-    // is at distance M + 1 <= 2^s, so none is farther
+    // Squaring passes double the exact horizon for V^3 each; Bellman-Ford
+    // sweeps (apsp_relax8_kernel) extend it by one hop for V^2 x in-degree
+    // each and stop by themselves at the fixpoint.  So: sweep to the
+    // fixpoint, capped at about one squaring pass's worth of sweeps; only a
+    // graph whose diameter outruns the cap gets a squaring pass (horizon x2)
+    // and sweeps again.  SDNROUTE_APSP_RELAX=0: squaring only, stopping when
+    // a pass changes nothing, or when after s squarings (exact for every
+    // distance <= 2^s) the largest finite distance M is < 2^s.
     const int nt = Vp / mt;
+    const char *rf = getenv("SDNROUTE_APSP_RELAX");
+    // the transposed 8-row block must fit LDS (16 B per vertex: V <= 10,240)
+    const bool relax = ctx->radj16 && ctx->max_indeg <= 64 && (size_t)V * 16 <= 160 * 1024 &&
+                       !(rf && !strcmp(rf, "0"));
+    // sweeps per squaring pass of cost: V^3 / (V E) = V / avg degree, /4
+    // for the sweeps' lower op rate (measured k=48: 46 us per sweep of all
+    // rows vs 0.95 ms per squaring pass)
+    long long capl = ctx->E > 0 ? ((long long)V * V) / (4ll * ctx->E) : 4;
+    const int cap = capl < 4 ? 4 : (capl > 64 ? 64 : (int)capl);
     ctx->last_launches = 0;
+    ctx->last_sweeps = 0;
+    if (relax) sdnr_allow_lds(reinterpret_cast<const void *>(apsp_relax8_kernel), (size_t)V * 16);
     for (int it = 1; it <= 40; ++it) {         // 2^40 >> any hop distance
+        if (relax) {
+            SDNR_HIP(hipMemsetAsync(changed, 0, 2 * sizeof(int), ctx->stream));
+            hipLaunchKernelGGL(apsp_relax8_kernel, dim3((V + 7) / 8), dim3(1024),
+                               (size_t)V * 16, ctx->stream, V, Vp, ctx->max_indeg, ctx->radj16,
+                               D, changed, cap);
+            SDNR_HIP(hipGetLastError());
+            int h[2] = {1, 0};
+            int rc = sdnr_fetch_ints(ctx, changed, 2, h);
+            if (rc) return rc;
+            ctx->last_sweeps += h[1];
+            if (!h[0]) break;                  // every row at its fixpoint: exact
+        }
         ctx->last_launches = it;
         SDNR_HIP(hipMemsetAsync(changed, 0, 2 * sizeof(int), ctx->stream));
         if (mt == MT64)
@@ -393,9 +528,10 @@ static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp, int m
                                D, changed);
         SDNR_HIP(hipGetLastError());
         int h[2] = {0, 0};
-        const int rc = sdnr_fetch_ints(ctx, changed, 2, h);
+        int rc = sdnr_fetch_ints(ctx, changed, 2, h);
         if (rc) return rc;
-        if (!h[0] || (it < 31 && (long long)h[1] < (1ll << it))) break;
+        if (!relax && (!h[0] || (it < 31 && (long long)h[1] < (1ll << it)))) break;
+        if (relax && !h[0]) break;             // nothing improved: exact
     }
     return SDNR_OK;
 }
@@ -424,6 +560,8 @@ int sdnr_launch_apsp(sdnr_ctx *ctx, uint16_t *d_dist)
         if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
         int rc = launch_apsp_squaring(ctx, D, V, Vp, mt);
         if (rc) return rc;
+        if (ctx->last_launches == 0 && ctx->last_sweeps > 0)
+            ctx->last_kernel = "apsp_relax8_kernel";   // converged by sweeps alone
         if (D != d_dist)
             SDNR_HIP(hipMemcpy2DAsync(d_dist, (size_t)V * 2, D, (size_t)Vp * 2, (size_t)V * 2, V,
                                       hipMemcpyDeviceToDevice, ctx->stream));
@@ -431,6 +569,7 @@ int sdnr_launch_apsp(sdnr_ctx *ctx, uint16_t *d_dist)
         return SDNR_OK;
     }
     ctx->last_kernel = "apsp_phase{1,2,3}_kernel";
+    ctx->last_sweeps = 0;
     ctx->last_launches = nb;
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
     hipLaunchKernelGGL(apsp_init_kernel, dim3(1024), dim3(256), 0, ctx->stream, V, Vp,

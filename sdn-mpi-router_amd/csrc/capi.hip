@@ -92,6 +92,12 @@ static void free_graph(sdnr_ctx *c)
     if (c->runs) (void)hipFree(c->runs);
     c->runs = nullptr;
     c->runs_R = 0;
+    if (c->adjb) (void)hipFree(c->adjb);
+    if (c->adjp) (void)hipFree(c->adjp);
+    if (c->radjx) (void)hipFree(c->radjx);
+    c->adjb = nullptr;
+    c->adjp = nullptr;
+    c->radjx = nullptr;
     if (c->adj16) (void)hipFree(c->adj16);
     if (c->deg32) (void)hipFree(c->deg32);
     if (c->radjw) (void)hipFree(c->radjw);
@@ -524,6 +530,46 @@ static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *
                 ctx->runs_R = R;
             }
         }
+        // bitmap rows + prefix counts + in-rows with vertex ids for the
+        // register-visited DFS (dfs_bits.hip): V <= 4096 (64 lanes x 64 bits)
+        const char *bf = getenv("SDNROUTE_BITS");                 // 0: off (A/B)
+        if (he == hipSuccess && maxin <= SDNR_WAVE && V <= 4096 && !(bf && !strcmp(bf, "0"))) {
+            std::vector<uint64_t> ab((size_t)V * SDNR_WAVE, 0ull);
+            std::vector<uint8_t> ap((size_t)V * SDNR_WAVE, 0);
+            for (int32_t u = 0; u < V; ++u)
+                for (int32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) {
+                    const int32_t v = col[e];
+                    ab[(size_t)u * SDNR_WAVE + (v >> 6)] |= 1ull << (v & 63);
+                }
+            for (int32_t u = 0; u < V; ++u) {
+                int run = 0;
+                for (int l = 0; l < SDNR_WAVE; ++l) {
+                    ap[(size_t)u * SDNR_WAVE + l] = (uint8_t)run;
+                    run += __builtin_popcountll(ab[(size_t)u * SDNR_WAVE + l]);
+                }
+            }
+            const std::vector<uint16_t> &in16 = sym ? a16 : r16;
+            const uint32_t dummyx = ((uint32_t)V + 31u) & ~31u;
+            std::vector<uint32_t> rx(((size_t)V + 1) * SDNR_WAVE);
+            for (size_t i = 0; i < rx.size(); ++i) {
+                const int x = in16[i];
+                rx[i] = x == V ? (dummyx + (uint32_t)(i % SDNR_WAVE)) | (0xFFFFu << 16)
+                               : (uint32_t)(x ^ ((x >> 3) & 31)) | ((uint32_t)x << 16);
+            }
+            he = hipMalloc(reinterpret_cast<void **>(&ctx->adjb), ab.size() * 8);
+            if (he == hipSuccess)
+                he = hipMemcpyAsync(ctx->adjb, ab.data(), ab.size() * 8, hipMemcpyHostToDevice,
+                                    ctx->stream);
+            if (he == hipSuccess) he = hipMalloc(reinterpret_cast<void **>(&ctx->adjp), ap.size());
+            if (he == hipSuccess)
+                he = hipMemcpyAsync(ctx->adjp, ap.data(), ap.size(), hipMemcpyHostToDevice,
+                                    ctx->stream);
+            if (he == hipSuccess) he = hipMalloc(reinterpret_cast<void **>(&ctx->radjx), rx.size() * 4);
+            if (he == hipSuccess)
+                he = hipMemcpyAsync(ctx->radjx, rx.data(), rx.size() * 4, hipMemcpyHostToDevice,
+                                    ctx->stream);
+            if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
+        }
         if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
         if (he != hipSuccess) {
             free_graph(ctx);
@@ -807,6 +853,59 @@ int sdnr_dfs_tables_slots(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc, uint3
     return run_sharded(ctx, src, nsrc, out, es, flags, shard_dfs_slots);
 }
 
+static int shard_tree_p16_h16(sdnr_ctx *c, const int32_t *ids, int32_t n, void *const o[3])
+{
+    return sdnr_launch_dfs(c, ids, n, nullptr, nullptr, static_cast<int32_t *>(o[1]),
+                           static_cast<uint32_t *>(o[0]), false, true);
+}
+
+static int shard_tree_p16_h32(sdnr_ctx *c, const int32_t *ids, int32_t n, void *const o[3])
+{
+    return sdnr_launch_dfs(c, ids, n, nullptr, nullptr, static_cast<int32_t *>(o[1]),
+                           static_cast<uint32_t *>(o[0]), false, false);
+}
+
+static int shard_tree_slot_h16(sdnr_ctx *c, const int32_t *ids, int32_t n, void *const o[3])
+{
+    return sdnr_launch_dfs(c, ids, n, nullptr, nullptr, static_cast<int32_t *>(o[1]),
+                           static_cast<uint32_t *>(o[0]), true, true);
+}
+
+static int shard_tree_slot_h32(sdnr_ctx *c, const int32_t *ids, int32_t n, void *const o[3])
+{
+    return sdnr_launch_dfs(c, ids, n, nullptr, nullptr, static_cast<int32_t *>(o[1]),
+                           static_cast<uint32_t *>(o[0]), true, false);
+}
+
+int sdnr_dfs_tables_tree(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc, uint32_t *tree,
+                         void *depth, int32_t layout, int32_t depth_bytes, uint32_t flags)
+{
+    int rc = begin_call(ctx, nsrc, src, flags, "sdnr_dfs_tables_tree");
+    if (rc) return rc;
+    if (nsrc > 0 && !tree) return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_tables_tree: null table");
+    if (layout == SDNR_TREE_PORT16) {
+        if (ctx->V > 0xFFFF || !ctx->port16)
+            return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_tables_tree: port16 needs V <= 65535 and "
+                             "ports < 0xFFFF (V=%d)", ctx->V);
+    } else if (layout == SDNR_TREE_SLOT) {
+        if (ctx->V > (1 << 26) - 1 || ctx->max_deg > 63)
+            return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_tables_tree: slots need V < 2^26 and rows "
+                             "of <= 63 links (V=%d, max degree %d)", ctx->V, ctx->max_deg);
+    } else {
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_tables_tree: layout %d", layout);
+    }
+    if (depth && depth_bytes != 2 && depth_bytes != 4)
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_tables_tree: depth_bytes %d", depth_bytes);
+    if (depth && depth_bytes == 2 && ctx->V > 0xFFFF)
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_tables_tree: u16 depths need V <= 65535");
+    void *const out[3] = {tree, depth, nullptr};
+    const size_t es[3] = {4, depth ? (size_t)depth_bytes : 0, 0};
+    const bool h16 = depth && depth_bytes == 2;
+    shard_launch_fn fn = layout == SDNR_TREE_SLOT ? (h16 ? shard_tree_slot_h16 : shard_tree_slot_h32)
+                                                  : (h16 ? shard_tree_p16_h16 : shard_tree_p16_h32);
+    return run_sharded(ctx, src, nsrc, out, es, flags, fn);
+}
+
 int sdnr_tree_pack(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port, int64_t n,
                    uint32_t *tree, int32_t layout, uint32_t flags)
 {
@@ -1036,6 +1135,14 @@ int sdnr_edge_ports(sdnr_ctx *ctx, const uint64_t *ends, int32_t nends, const ui
 }
 
 const char *sdnr_last_kernel(const sdnr_ctx *ctx) { return ctx ? ctx->last_kernel : ""; }
+
+int sdnr_last_sweeps(const sdnr_ctx *ctx, int32_t *sweeps)
+{
+    CHECK_CTX(ctx);
+    if (!sweeps) return sdnr_fail(SDNR_ERR_INVAL, "sdnr_last_sweeps: null out");
+    *sweeps = ctx->last_sweeps;
+    return SDNR_OK;
+}
 
 int sdnr_last_launches(const sdnr_ctx *ctx, int32_t *launches)
 {

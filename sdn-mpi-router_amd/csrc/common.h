@@ -68,6 +68,14 @@ struct sdnr_ctx {
     // of start | stride << 16 | count << 25
     uint32_t *runs = nullptr;
     int32_t runs_R = 0;
+    // bitmap rows for the register-visited DFS (dfs_bits.hip, V <= 4096):
+    // adjb[u * 64 + l] = bits of u's out-neighbours 64l..64l+63, adjp the
+    // exclusive prefix popcount of lane blocks (u8), radjx[v * 64 + i] =
+    // swizzled count index | in-neighbour << 16 (padding: dummy | 0xFFFF << 16;
+    // row V all padding)
+    uint64_t *adjb = nullptr;
+    uint8_t *adjp = nullptr;
+    uint32_t *radjx = nullptr;
 
     // grow-only device scratch / staging
     void *scratch = nullptr;
@@ -84,6 +92,7 @@ struct sdnr_ctx {
     bool timed = false;
     const char *last_kernel = "";       // variant launched by the last table call
     int32_t last_launches = 0;          // main-kernel launches of the last table call
+    int32_t last_sweeps = 0;            // Bellman-Ford sweeps of the last APSP call
     int32_t plane_depth = 0;            // levels the bit-plane BFS last needed on this graph
     int *d_err = nullptr;               // kernel watchdog word (0 = ok)
     int *h_flag = nullptr;              // pinned host words for level-loop checks
@@ -129,10 +138,15 @@ int sdnr_fetch_ints(sdnr_ctx *ctx, const int *d_src, int n, int *out);
 int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
                     int32_t *d_parent, int32_t *d_port, int32_t *d_hops,
                     uint32_t *d_tree,         // d_tree: packed layout instead of the three
-                    bool slots = false);      // d_tree as parent | slot << 26
+                    bool slots = false,       // d_tree as parent | slot << 26
+                    bool hops16 = false);     // d_hops as u16 (0xFFFF unreached)
 // int32 trees -> parent | port << 16 or parent | slot << 26 (dfs.hip)
 int sdnr_launch_tree_pack(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port, size_t n,
                           uint32_t *tree, bool slots);
+// register-visited DFS (dfs_bits.hip): V <= 4096 with bitmap rows uploaded
+bool sdnr_dfs_bits_ok(const sdnr_ctx *ctx);
+int sdnr_launch_dfs_bits(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, int32_t *d_parent,
+                         int32_t *d_port, int32_t *d_hops, uint32_t *d_tree, bool hops16);
 // LDS-row DFS (dfs_runs.hip): usable when the run-encoded rows plus one
 // source's state fit a workgroup's LDS
 bool sdnr_dfs_runs_ok(const sdnr_ctx *ctx, bool hops);

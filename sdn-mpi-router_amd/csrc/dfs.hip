@@ -1060,6 +1060,16 @@ constexpr int kSplitQ = 64;                    // queued records per search wave
 constexpr int kFlagPrio = 1, kFlagNT = 2, kFlagNoStore = 4, kFlagNoPort = 8;
 // dfs_async_kernel: the worker rows are pre-swizzled count indices (radjw)
 constexpr int kFlagPreSwz = 16;
+// hop counts written as u16 (0xFFFF unreached) instead of int32: the depth
+// plane of the drop-in's table pool (sdnr_dfs_tables_tree)
+constexpr int kFlagHops16 = 32;
+
+// hop count of entry e of an [rows][V] hop table, int32 or u16 (kFlagHops16)
+__device__ __forceinline__ void put_hop(int32_t *__restrict__ hops, size_t e, int h, int flags)
+{
+    if (flags & kFlagHops16) reinterpret_cast<uint16_t *>(hops)[e] = (uint16_t)h;
+    else hops[e] = h;
+}
 
 template <int FMT>
 __device__ __forceinline__ int split_row(const void *__restrict__ rows,
@@ -1153,6 +1163,7 @@ __device__ __forceinline__ void split_writer(int V, int W, const int32_t *__rest
                         const int32_t tv = (int32_t)((uint32_t)par | ((uint32_t)slot << 26));
                         if (flags & kFlagNT) __builtin_nontemporal_store(tv, &out_parent[e]);
                         else if (!(flags & kFlagNoStore)) out_parent[e] = tv;
+                        if (HOPS && !(flags & kFlagNoStore)) put_hop(out_hops, e, (int)qdep[at], flags);
                     } else {
                         const int pt = (flags & kFlagNoPort) ? slot
                                                              : ell_port[(size_t)par * W + slot];
@@ -1167,7 +1178,13 @@ __device__ __forceinline__ void split_writer(int V, int W, const int32_t *__rest
                                 __builtin_nontemporal_store(par, &out_parent[e]);
                                 __builtin_nontemporal_store(pt, &out_port[e]);
                             }
-                            if (HOPS) __builtin_nontemporal_store((int)qdep[at], &out_hops[e]);
+                            if (HOPS) {
+                                if (flags & kFlagHops16)
+                                    __builtin_nontemporal_store(
+                                        (uint16_t)qdep[at], reinterpret_cast<uint16_t *>(out_hops) + e);
+                                else
+                                    __builtin_nontemporal_store((int)qdep[at], &out_hops[e]);
+                            }
                         } else {
                             if (PACKED) {
                                 out_parent[e] = (int32_t)(((uint32_t)par & 0xFFFFu) |
@@ -1176,7 +1193,7 @@ __device__ __forceinline__ void split_writer(int V, int W, const int32_t *__rest
                                 out_parent[e] = par;
                                 out_port[e] = pt;
                             }
-                            if (HOPS) out_hops[e] = (int)qdep[at];
+                            if (HOPS) put_hop(out_hops, e, (int)qdep[at], flags);
                         }
                     }
                 }
@@ -1257,12 +1274,12 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
             const int s = uniform(src[si]);
             int32_t *prow = out_parent + (size_t)si * V;
             int32_t *trow = PACKED ? nullptr : out_port + (size_t)si * V;
-            int32_t *hrow = HOPS ? out_hops + (size_t)si * V : nullptr;
+            const size_t hb = (size_t)si * V;        // row of the hop table
             if (s < 0 || s >= V) {                 // unknown source: empty row
                 for (int v = lane; v < V; v += SDNR_WAVE) {
                     prow[v] = -1;                  // packed: 0xFFFFFFFF
                     if (!PACKED) trow[v] = -1;
-                    if (HOPS) hrow[v] = -1;
+                    if (HOPS) put_hop(out_hops, hb + v, -1, flags);
                 }
                 continue;
             }
@@ -1272,7 +1289,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                 prow[s] = PK == kTreePort16 ? (int32_t)((uint32_t)s | 0xFFFF0000u)
                         : PK == kTreeSlot  ? (int32_t)((uint32_t)s | (63u << 26)) : s;
                 if (!PACKED) trow[s] = -1;
-                if (HOPS) hrow[s] = 0;
+                if (HOPS) put_hop(out_hops, hb + s, 0, flags);
                 ring[0] = RE::put((uint32_t)s, 0u);
                 __hip_atomic_store(&ctl[2 * NS + w], si, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1442,7 +1459,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                 if (((vis[vsw(v >> 5)] >> (v & 31)) & 1u) == 0u) {
                     prow[v] = -1;
                     if (!PACKED) trow[v] = -1;
-                    if (HOPS) hrow[v] = -1;
+                    if (HOPS) put_hop(out_hops, hb + v, -1, flags);
                 }
             }
         }
@@ -1547,12 +1564,12 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
         const int s = uniform(src[si]);
         int32_t *prow = out_parent + (size_t)si * V;
         int32_t *trow = PACKED ? nullptr : out_port + (size_t)si * V;
-        int32_t *hrow = HOPS ? out_hops + (size_t)si * V : nullptr;
+        const size_t hb = (size_t)si * V;        // row of the hop table
         if (s < 0 || s >= V) {
             for (int v = threadIdx.x; v < V; v += blockDim.x) {
                 prow[v] = -1;                    // packed: 0xFFFFFFFF
                 if (!PACKED) trow[v] = -1;
-                if (HOPS) hrow[v] = -1;
+                if (HOPS) put_hop(out_hops, hb + v, -1, flags);
             }
             continue;
         }
@@ -1734,6 +1751,13 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                     __builtin_amdgcn_s_sleep(1);
                 }
                 uint32_t cc = 0u;
+                // the children's counts are read FIRST: LDS ops complete in
+                // order, so behind the mark / stack / ring / parent writes the
+                // gather waited for all four; issued before them it returns
+                // while they drain (the next row wait hides them)
+#ifndef SDNR_AB_WRITES_FIRST
+                if (fresh) cc = cnt_of(x);
+#endif
                 if (fresh) {
                     atomicOr(&vis[x >> 5], 1u << (x & 31));
                     if (C16) {
@@ -1745,19 +1769,20 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                     if (HOPS) dep[x] = (uint16_t)(du + 1);
                     stk[sp + rank] = (uint16_t)x;
                     ring[(pub + rank) & (RING - 1)] = (uint16_t)x;
-                    // children-first: the new stack top is these children
-                    // (highest id on top); their counts are read while the
-                    // prefetched rows are still in flight
+#ifdef SDNR_AB_WRITES_FIRST   // A/B build: the round-3 push (count after the writes)
                     cc = cnt_of(x);
+#endif
                 }
-                const uint64_t mc = __ballot(cc != 0u);
                 pub += c;
-                // announce the children: the count gather above waited for
-                // the ring writes (LDS ops complete in order), so an LDS-only
-                // release suffices and does not wait for the row prefetches
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                // announce the children without waiting for the writes: one
+                // wave's LDS ops execute in issue order, so a worker that
+                // reads the new count reads the ring after its entries were
+                // written; the empty asm keeps the compiler from moving the
+                // store above them
+                __asm__ volatile("" ::: "memory");
                 if (lane == 0) __hip_atomic_store(&ctl[0], pub, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                const uint64_t mc = __ballot(cc != 0u);
                 pubd = pub;
                 if (mc) {
                     // children above the highest one with a count are leaves
@@ -1900,7 +1925,8 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                         prow[v] = p[k];
                         trow[v] = pt[k];
                     }
-                    if (HOPS) hrow[v] = p[k] < 0 ? -1 : (v == s ? 0 : (int)dep[v]);
+                    if (HOPS) put_hop(out_hops, hb + v, p[k] < 0 ? -1 : (v == s ? 0 : (int)dep[v]),
+                                      flags);
                 }
             }
         }
@@ -2202,13 +2228,14 @@ static bool split_ok()
 // the end event itself
 template <int NS>
 static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, int32_t *d_parent,
-                           int32_t *d_port, int32_t *d_hops, uint32_t *d_tree, int tree);
+                           int32_t *d_port, int32_t *d_hops, uint32_t *d_tree, int tree,
+                           int hflags);
 
 // search waves per workgroup: 7 on sparse tori (4 workgroups of 8 waves fill
 // a CU's 32 wave slots with 28 sources), else 3 (LDS-bound: Jellyfish fits 3
 // workgroups of 3 sources); SDNROUTE_DFS_SPLIT_NS=3|7 overrides
 static int launch_split(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, int32_t *d_parent,
-                        int32_t *d_port, int32_t *d_hops, uint32_t *d_tree, int tree)
+                        int32_t *d_port, int32_t *d_hops, uint32_t *d_tree, int tree, int hflags)
 {
     int ns = ctx->W <= 8 && packed_j8(ctx->V) == 1 ? 7 : 3;
     if (ctx->W > 8 && ctx->W <= 16) {
@@ -2230,16 +2257,21 @@ static int launch_split(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, int32
         if ((k == 5 || k == 11) && ctx->W > 8 && ctx->W <= 16) ns = k;   // rows of 9-16 slots
     }
     switch (ns) {
-    case 7: return launch_split_ns<7>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree, tree);
-    case 5: return launch_split_ns<5>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree, tree);
-    case 11: return launch_split_ns<11>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree, tree);
-    default: return launch_split_ns<3>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree, tree);
+    case 7: return launch_split_ns<7>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree, tree,
+                                     hflags);
+    case 5: return launch_split_ns<5>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree, tree,
+                                     hflags);
+    case 11: return launch_split_ns<11>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree, tree,
+                                      hflags);
+    default: return launch_split_ns<3>(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree, tree,
+                                     hflags);
     }
 }
 
 template <int NS>
 static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, int32_t *d_parent,
-                           int32_t *d_port, int32_t *d_hops, uint32_t *d_tree, int tree)
+                           int32_t *d_port, int32_t *d_hops, uint32_t *d_tree, int tree,
+                           int hflags)
 {
     const int V = ctx->V, W = ctx->W;
     const bool packed = d_tree != nullptr, hops = d_hops != nullptr;
@@ -2255,8 +2287,8 @@ static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, in
     const int fmt = ctx->ell16 && V <= 65535 ? kRow16 : (ctx->ell16 && ctx->ell_hi ? kRow17 : kRow32);
     if (tree == kTreePort16 && fmt != kRow16)
         return sdnr_fail(SDNR_ERR_INVAL, "dfs split: packed tables need V <= 65535");
-    if (tree == kTreeSlot && hops)
-        return sdnr_fail(SDNR_ERR_INVAL, "dfs split: slot trees carry no hop counts");
+    if (tree == kTreeSlot && hops && fmt == kRow32)
+        return sdnr_fail(SDNR_ERR_INVAL, "dfs split: slot trees with hop counts need V < 131071");
     const size_t lds = split_lds_words(V, ring, NS, hops, lpr) * 4;
     if (lds > SDNR_MAX_LDS_PER_BLOCK)
         return sdnr_fail(SDNR_ERR_INVAL, "graph too large for the LDS visited sets (V=%d)", V);
@@ -2281,7 +2313,7 @@ static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, in
     // rows of 9-16 slots (Jellyfish): search waves issue at raised priority
     // over their writer (measured 1.027 -> 0.973 s on the 100k Jellyfish; the
     // torus rows of 6 slots measured 3 % slower with it, so not there)
-    const int flags = dfs_flags(lpr == 16 ? kFlagPrio : 0);
+    const int flags = dfs_flags(lpr == 16 ? kFlagPrio : 0) | hflags;
 #define SDNR_SPLIT(L_, J_, R_, H_, F_, P_)                                                    \
     do {                                                                                     \
         auto k = dfs_split_kernel<L_, J_, H_, R_, NS, F_, P_>;                               \
@@ -2292,13 +2324,11 @@ static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, in
     } while (0)
 #define SDNR_SPLIT_F(L_, J_, R_, H_)                                                          \
     do {                                                                                     \
-        if constexpr (!H_) {                                                                 \
-            if (tree == kTreeSlot) {                                                         \
-                if (fmt == kRow16) SDNR_SPLIT(L_, J_, R_, H_, kRow16, kTreeSlot);            \
-                else if (fmt == kRow17) SDNR_SPLIT(L_, J_, R_, H_, kRow17, kTreeSlot);       \
-                else SDNR_SPLIT(L_, J_, R_, H_, kRow32, kTreeSlot);                          \
-                break;                                                                       \
-            }                                                                                \
+        if (tree == kTreeSlot) {                                                             \
+            if (fmt == kRow16) SDNR_SPLIT(L_, J_, R_, H_, kRow16, kTreeSlot);                \
+            else if (fmt == kRow17) SDNR_SPLIT(L_, J_, R_, H_, kRow17, kTreeSlot);           \
+            else if constexpr (!H_) SDNR_SPLIT(L_, J_, R_, H_, kRow32, kTreeSlot);           \
+            break;                                                                           \
         }                                                                                    \
         if (fmt == kRow16 && packed) SDNR_SPLIT(L_, J_, R_, H_, kRow16, kTreePort16);        \
         else if (fmt == kRow16) SDNR_SPLIT(L_, J_, R_, H_, kRow16, kTreeInt32);              \
@@ -2341,9 +2371,25 @@ int sdnr_launch_tree_pack(sdnr_ctx *ctx, const int32_t *parent, const int32_t *p
     return SDNR_OK;
 }
 
+// the register-visited kernel (dfs_bits.hip) where it applies: forced with
+// SDNROUTE_DFS_STRATEGY=bits (A/B; not yet the default)
+static bool dfs_bits_default(const char *force)
+{
+    return force && !strcmp(force, "bits");
+}
+
+// hop counts as u16 (0xFFFF unreached) into d_hops
+__global__ __launch_bounds__(256) void dfs_hops16_kernel(size_t n, const int32_t *__restrict__ h,
+                                                         uint16_t *__restrict__ out)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        out[i] = (uint16_t)h[i];
+}
+
 int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
                     int32_t *d_parent, int32_t *d_port, int32_t *d_hops, uint32_t *d_tree,
-                    bool slots)
+                    bool slots, bool hops16)
 {
     const int V = ctx->V;
     if (nsrc == 0 || V == 0) return SDNR_OK;
@@ -2393,22 +2439,47 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
         return SDNR_OK;
     }
+    // bitmap rows, visited set in registers (dfs_bits.hip): V <= 4096;
+    // SDNROUTE_DFS_STRATEGY=bits forces it (A/B), =async the round-3 kernel
+    if (!slots && sdnr_dfs_bits_ok(ctx) && dfs_bits_default(force)) {
+        int rc = sdnr_launch_dfs_bits(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree, hops16);
+        if (rc) return rc;
+        if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+        return SDNR_OK;
+    }
     const bool count_ok = ctx->adj16 != nullptr && ctx->radj16 != nullptr && V < 65535 &&
                           dfs_lds_bytes_count(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;
     const bool async_ok = count_ok && dfs_lds_bytes_async(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;
     const bool async = async_ok && (force ? !strcmp(force, "async") : small);
     slots = slots && packed;
+    const int hflags = hops && hops16 ? kFlagHops16 : 0;
     if (!async && !small && ell && ctx->W <= 32 && packed_ok() && split_ok() &&
-        (!packed || slots || (ctx->ell16 && V <= 65535)))
+        (!packed || slots || (ctx->ell16 && V <= 65535)) &&
+        !(slots && hops && !(ctx->ell16 && (V <= 65535 || ctx->ell_hi))))
         return launch_split(ctx, d_src, nsrc, d_parent, d_port, d_hops, d_tree,
-                            slots ? kTreeSlot : (packed ? kTreePort16 : kTreeInt32));
-    if (packed && (!async || slots)) {
-        // no such epilogue in this strategy: int32 tables into scratch, then pack
+                            slots ? kTreeSlot : (packed ? kTreePort16 : kTreeInt32), hflags);
+    if ((packed && (!async || slots)) || (hops && hops16 && !async)) {
+        // no such epilogue in this strategy: int32 tables into scratch, then
+        // pack (and narrow the hop counts)
         const size_t n = (size_t)nsrc * (size_t)V;
-        int rc = sdnr_reserve(&ctx->scratch2, &ctx->scratch2_bytes, 2 * n * sizeof(int32_t));
+        const bool h16 = hops && hops16;
+        int rc = sdnr_reserve(&ctx->scratch2, &ctx->scratch2_bytes,
+                              (h16 ? 3 : 2) * n * sizeof(int32_t));
         if (rc) return rc;
         int32_t *tp = static_cast<int32_t *>(ctx->scratch2);
-        if ((rc = sdnr_launch_dfs(ctx, d_src, nsrc, tp, tp + n, nullptr, nullptr))) return rc;
+        int32_t *th = h16 ? tp + 2 * n : d_hops;
+        if (!packed) {                           // int32 tables, u16 hop counts
+            if ((rc = sdnr_launch_dfs(ctx, d_src, nsrc, d_parent, d_port, tp, nullptr))) return rc;
+            hipLaunchKernelGGL(dfs_hops16_kernel, dim3(ctx->num_cus * 8), dim3(256), 0,
+                               ctx->stream, n, tp, reinterpret_cast<uint16_t *>(d_hops));
+            SDNR_HIP(hipGetLastError());
+            if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+            return SDNR_OK;
+        }
+        if ((rc = sdnr_launch_dfs(ctx, d_src, nsrc, tp, tp + n, th, nullptr))) return rc;
+        if (h16)
+            hipLaunchKernelGGL(dfs_hops16_kernel, dim3(ctx->num_cus * 8), dim3(256), 0,
+                               ctx->stream, n, th, reinterpret_cast<uint16_t *>(d_hops));
         if (slots)
             hipLaunchKernelGGL(dfs_slot_pack_kernel, dim3(ctx->num_cus * 8), dim3(256), 0,
                                ctx->stream, n, V, tp, ctx->row_ptr, ctx->col, d_tree);
@@ -2444,7 +2515,7 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         const char *pz = getenv("SDNROUTE_DFS_PRESWZ");
         const uint16_t *rw = c16 ? ctx->radjc : ctx->radjw;
         const bool preswz = rw && !(pz && !strcmp(pz, "0"));
-        const int aflags = dfs_flags(kFlagPrio) | (preswz ? kFlagPreSwz : 0);
+        const int aflags = dfs_flags(kFlagPrio) | (preswz ? kFlagPreSwz : 0) | hflags;
         // paired worker rows (in-degree <= 32, pre-swizzled rows only)
         const bool pair = preswz && ctx->radj_pair;
         int cgrid = (int)((size_t)ctx->num_cus * cpc);
@@ -2477,7 +2548,16 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
                                            "dfs_async_kernel<6,packed>", "",
                                            "dfs_async_kernel<8,packed>"};
             ctx->last_kernel = pnames[nw];
-            if (nw == 2) SDNR_ASYNC_P(2, false, true);
+            if (hops) {                          // the drop-in's pool: tree words + depth
+                static const char *hnames[] = {"", "", "", "dfs_async_kernel<3,packed,hops>",
+                                               "dfs_async_kernel<4,packed,hops>", "",
+                                               "dfs_async_kernel<6,packed,hops>"};
+                const int hw = nw <= 3 ? 3 : (nw >= 6 ? 6 : 4);
+                ctx->last_kernel = hnames[hw];
+                if (hw == 3) SDNR_ASYNC_P(3, true, true);
+                else if (hw == 6) SDNR_ASYNC_P(6, true, true);
+                else SDNR_ASYNC_P(4, true, true);
+            } else if (nw == 2) SDNR_ASYNC_P(2, false, true);
             else if (nw == 3) SDNR_ASYNC_P(3, false, true);
             else if (nw == 5) SDNR_ASYNC_P(5, false, true);
             else if (nw == 6) SDNR_ASYNC_P(6, false, true);

@@ -239,6 +239,172 @@ __global__ __launch_bounds__(256) void route_jump_packed_kernel(
     }
 }
 
+// inclusive prefix sum across the 64 lanes of a wave
+__device__ __forceinline__ int wave_incl_scan(int x)
+{
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(x, o, 64);
+        if (lane >= o) x += t;
+    }
+    return x;
+}
+
+// Output-centric expansion (the default for packed trees).  Consecutive
+// pairs very often ask for the same (tree row, destination switch) -- every
+// host on a switch has the same route from a given source switch, and the
+// requests of an all-pairs or rank-pair set come ordered by source, then
+// destination -- and then their entries are identical except the last one
+// (the destination host's port).  Each wave takes up to 64 consecutive pairs
+// (as many as their DISTINCT paths fit its CAP-entry LDS buffer), walks each
+// distinct path once into LDS (16 lanes per path, the 2^j-th-ancestor jumps
+// of route_jump_packed_kernel), then writes the pairs' entries in order: the
+// output range of the group [off[first], off[last + 1]) is contiguous, so the
+// stores fill whole cache lines, and the tree gathers drop from one per entry
+// to one per distinct path entry.  A pair whose path alone exceeds CAP is
+// walked straight to global memory (16 lanes, as the jump kernel).
+template <int CAP>
+__global__ __launch_bounds__(256) void route_seg_packed_kernel(
+    int V, const uint32_t *__restrict__ tree, Anc16 anc,
+    const int32_t *__restrict__ rows, const int32_t *__restrict__ dsts,
+    const int32_t *__restrict__ last_port, int npairs, const int64_t *__restrict__ off,
+    int32_t *__restrict__ hop_switch, int32_t *__restrict__ hop_port)
+{
+    __shared__ uint32_t seg_lds[4][CAP];
+    __shared__ int lp_lds[4][64];
+    const int lane = lane_id();
+    const int wv = threadIdx.x >> 6;
+    uint32_t *buf = seg_lds[wv];
+    int *lps = lp_lds[wv];
+    const int groups = (npairs + 63) >> 6;
+    const int nwaves = gridDim.x * 4;
+    const uint16_t *__restrict__ anc16 = anc.a[4];
+    for (int g = blockIdx.x * 4 + wv; g < groups; g += nwaves) {
+        const int gend = min(npairs, (g + 1) * 64);
+        for (int base = g * 64; base < gend;) {
+            const int i = base + lane;
+            const bool valid = i < gend;
+            int r = -1, d = -1, lp = 0;
+            int64_t lo = 0;
+            int L = 0;
+            if (valid) {
+                r = rows[i];
+                d = dsts[i];
+                lp = last_port[i];
+                lo = off[i];
+                L = (int)(off[i + 1] - lo);
+            }
+            const int pl = L > 0 ? L - 1 : 0;       // path entries before the last
+            const int pr = __shfl_up(r, 1, 64), pd = __shfl_up(d, 1, 64);
+            const bool head = valid && (lane == 0 || pr != r || pd != d);
+            const int c = head ? pl : 0;
+            const int incl = wave_incl_scan(c);
+            const int segoff = head ? incl - c : incl - pl;   // followers share the head's
+            const uint64_t fit = __ballot(valid && incl <= CAP);
+            int n = fit == ~0ull ? 64 : __builtin_ctzll(~fit);   // leading lanes that fit
+            if (n == 0) {
+                // one pair longer than the buffer: walk it straight to global
+                const int64_t lo0 = (int64_t)(uint32_t)read_lane((int)lo, 0) |
+                                    ((int64_t)read_lane((int)(lo >> 32), 0) << 32);
+                const int h = read_lane(pl, 0);
+                const int r0 = read_lane(r, 0);
+                const size_t rb = (size_t)r0 * V;
+                if (lane < 16) {
+                    const int k = lane;
+                    int y = read_lane(d, 0);
+                    if (k == 0) {
+                        hop_switch[lo0 + h] = y;
+                        hop_port[lo0 + h] = read_lane(lp, 0);
+                    }
+                    if (k < h) {
+                        if (k & 1) y = (int)(tree[rb + y] & 0xFFFFu);
+#pragma unroll
+                        for (int j = 1; j < 4; ++j)
+                            if (k & (1 << j)) y = anc.a[j][rb + y];
+                        for (int u = k; u < h; u += 16) {
+                            const uint32_t e = tree[rb + y];
+                            hop_switch[lo0 + h - u - 1] = (int32_t)(e & 0xFFFFu);
+                            hop_port[lo0 + h - u - 1] = (int32_t)(e >> 16);
+                            if (u + 16 < h) y = anc16[rb + y];
+                        }
+                    }
+                }
+                base += 1;
+                continue;
+            }
+            // distinct paths of the n pairs, 4 at a time (16 lanes each)
+            uint64_t heads = __ballot(head && lane < n && pl > 0);
+            while (heads) {
+                // the q-th lowest head for lane group q
+                const int q = lane >> 4, k = lane & 15;
+                uint64_t hm = heads;
+                for (int t = 0; t < q && hm; ++t) hm &= hm - 1;
+                const int hl = hm ? __builtin_ctzll(hm) : -1;
+                const int src_lane = hl < 0 ? 0 : hl;
+                const int hr = __shfl(r, src_lane, 64), hd = __shfl(d, src_lane, 64);
+                const int h = __shfl(pl, src_lane, 64), so = __shfl(segoff, src_lane, 64);
+                if (hl >= 0 && k < h) {
+                    const size_t rb = (size_t)hr * V;
+                    int y = hd;
+                    if (k & 1) y = (int)(tree[rb + y] & 0xFFFFu);
+#pragma unroll
+                    for (int j = 1; j < 4; ++j)
+                        if (k & (1 << j)) y = anc.a[j][rb + y];
+                    for (int u = k; u < h; u += 16) {
+                        buf[so + h - u - 1] = tree[rb + y];
+                        if (u + 16 < h) y = anc16[rb + y];
+                    }
+                }
+                for (int t = 0; t < 4 && heads; ++t) heads &= heads - 1;
+            }
+            lps[lane] = lp;                          // last ports, read by entry
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // the pairs' entries, in output order, one run of equal (row,
+            // destination) pairs at a time: the run's entries are cnt copies
+            // of one L-entry route, contiguous, so the lanes stream them with
+            // full-wave stores (pair q, entry k of flat index t = q L + k)
+            uint64_t runs = __ballot(head && lane < n);
+            while (runs) {
+                const int p0 = __builtin_ctzll(runs);
+                runs &= runs - 1;
+                const int p1 = runs ? __builtin_ctzll(runs) : n;
+                const int Lr = read_lane(L, p0);
+                if (Lr <= 0) continue;
+                const int64_t lop = (int64_t)(uint32_t)read_lane((int)lo, p0) |
+                                    ((int64_t)read_lane((int)(lo >> 32), p0) << 32);
+                const int sop = read_lane(segoff, p0), dp = read_lane(d, p0);
+                const int total = (p1 - p0) * Lr;
+                const float inv = 1.0f / (float)Lr;
+                for (int t0 = 0; t0 < total; t0 += 64) {
+                    const int t = t0 + lane;
+                    if (t < total) {
+                        int q = (int)((float)t * inv);
+                        int k = t - q * Lr;
+                        if (k >= Lr) { ++q; k -= Lr; }
+                        if (k < 0) { --q; k += Lr; }
+                        int sw, pt;
+                        if (k < Lr - 1) {
+                            const uint32_t e = buf[sop + k];
+                            sw = (int)(e & 0xFFFFu);
+                            pt = (int)(e >> 16);
+                        } else {
+                            sw = dp;
+                            pt = lps[p0 + q];
+                        }
+                        hop_switch[lop + t] = sw;
+                        hop_port[lop + t] = pt;
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();        // buffer reused by the next group
+            base += n;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void route_walk_kernel(
     int V, const int32_t *__restrict__ parent, const int32_t *__restrict__ port,
     const int32_t *__restrict__ rows, const int32_t *__restrict__ dsts,
@@ -348,12 +514,23 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
                                ctx->V, n, prev, prev, o);
             tabs.a[j] = o;
         }
-        int64_t g = ((int64_t)npairs * 16 + 255) / 256;
-        if (g > ctx->num_cus * 16) g = ctx->num_cus * 16;
-        ctx->last_kernel = "route_jump_packed_kernel<16>";
-        hipLaunchKernelGGL(route_jump_packed_kernel<16>, dim3((unsigned)g), dim3(256), 0,
-                           ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts, d_last_port, npairs,
-                           d_off, d_switch, d_hport);
+        const char *sg = getenv("SDNROUTE_ROUTE_SEG");        // "0": per-entry jump walks
+        if (!(sg && !strcmp(sg, "0"))) {
+            // 4 waves per workgroup, one 64-pair group per wave at a time
+            int64_t g = (((int64_t)npairs + 63) / 64 + 3) / 4;
+            if (g > ctx->num_cus * 8) g = ctx->num_cus * 8;
+            ctx->last_kernel = "route_seg_packed_kernel<1024>";
+            hipLaunchKernelGGL(route_seg_packed_kernel<1024>, dim3((unsigned)g), dim3(256), 0,
+                               ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts, d_last_port,
+                               npairs, d_off, d_switch, d_hport);
+        } else {
+            int64_t g = ((int64_t)npairs * 16 + 255) / 256;
+            if (g > ctx->num_cus * 16) g = ctx->num_cus * 16;
+            ctx->last_kernel = "route_jump_packed_kernel<16>";
+            hipLaunchKernelGGL(route_jump_packed_kernel<16>, dim3((unsigned)g), dim3(256), 0,
+                               ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts, d_last_port,
+                               npairs, d_off, d_switch, d_hport);
+        }
     } else if (serial) {
         int g = (npairs + 255) / 256;
         if (g > ctx->num_cus * 16) g = ctx->num_cus * 16;

@@ -36,10 +36,11 @@ EXPORTED_SYMBOLS = (
     "sdnr_abi_version", "sdnr_last_error", "sdnr_device_count", "sdnr_create",
     "sdnr_create_multi", "sdnr_device_list", "sdnr_destroy", "sdnr_set_stream", "sdnr_synchronize", "sdnr_graph_upload",
     "sdnr_graph_info", "sdnr_dfs_tables", "sdnr_dfs_tables_packed", "sdnr_dfs_tables_slots",
-    "sdnr_tree_pack", "sdnr_shortest_tables",
+    "sdnr_dfs_tables_tree", "sdnr_tree_pack", "sdnr_shortest_tables",
     "sdnr_apsp", "sdnr_route_offsets", "sdnr_route_expand", "sdnr_ecmp_counts",
     "sdnr_ecmp_routes",
-    "sdnr_last_kernel_ms", "sdnr_last_kernel", "sdnr_last_launches", "sdnr_edge_ports",
+    "sdnr_last_kernel_ms", "sdnr_last_kernel", "sdnr_last_launches", "sdnr_last_sweeps",
+    "sdnr_edge_ports",
 )
 
 
@@ -80,6 +81,7 @@ def _bind(L):
         "sdnr_dfs_tables_packed": ([vp, vp, i32, vp, u32], c_int),
         "sdnr_dfs_tables_slots": ([vp, vp, i32, vp, u32], c_int),
         "sdnr_tree_pack": ([vp, vp, vp, ctypes.c_int64, vp, i32, u32], c_int),
+        "sdnr_dfs_tables_tree": ([vp, vp, i32, vp, vp, i32, i32, u32], c_int),
         "sdnr_shortest_tables": ([vp, vp, i32, vp, vp, vp, u32], c_int),
         "sdnr_apsp": ([vp, vp, u32], c_int),
         "sdnr_route_offsets": ([vp, vp, i32, vp, vp, i32, vp, u32], c_int),
@@ -89,6 +91,7 @@ def _bind(L):
         "sdnr_last_kernel_ms": ([vp, ctypes.POINTER(ctypes.c_float)], c_int),
         "sdnr_last_kernel": ([vp], ctypes.c_char_p),
         "sdnr_last_launches": ([vp, ctypes.POINTER(i32)], c_int),
+        "sdnr_last_sweeps": ([vp, ctypes.POINTER(i32)], c_int),
         "sdnr_edge_ports": ([vp, vp, i32, vp, i32, vp, u32], c_int),
     }
     for name, (args, res) in sig.items():
@@ -382,6 +385,28 @@ class Context(object):
         _check(self._lib.sdnr_dfs_tables_slots(self._h, ctypes.c_void_p(src_ptr), int(nsrc),
                                                ctypes.c_void_p(tree_ptr), flags))
 
+    def dfs_tables_tree_device(self, src_ptr, nsrc, tree_ptr, depth_ptr, layout, depth_bytes,
+                               timing=False):
+        """Trees in a 4-byte layout (TREE_PORT16 / TREE_SLOT) plus depths
+        (u16 or int32, ``depth_bytes`` 2 / 4; depth_ptr 0: none) straight
+        from the DFS kernels (sdnr_dfs_tables_tree)."""
+        flags = DEVICE_PTRS | (TIMING if timing else 0)
+        _check(self._lib.sdnr_dfs_tables_tree(
+            self._h, ctypes.c_void_p(src_ptr), int(nsrc), ctypes.c_void_p(tree_ptr),
+            ctypes.c_void_p(depth_ptr) if depth_ptr else None, int(layout), int(depth_bytes),
+            flags))
+
+    def dfs_tables_tree(self, srcs, layout, depth_bytes=2):
+        """Host-buffer form of dfs_tables_tree_device: (tree uint32 [S, V],
+        depth uint16 / int32 [S, V])."""
+        srcs = np.ascontiguousarray(srcs, np.int32)
+        S, V = int(srcs.shape[0]), self.V
+        tree = np.empty((S, V), np.uint32)
+        depth = np.empty((S, V), np.uint16 if depth_bytes == 2 else np.int32)
+        _check(self._lib.sdnr_dfs_tables_tree(self._h, _ptr(srcs), S, _ptr(tree), _ptr(depth),
+                                              int(layout), int(depth_bytes), 0))
+        return tree, depth
+
     def tree_pack_device(self, parent_ptr, port_ptr, n, tree_ptr, layout):
         """int32 parent/port tables (device) -> 4-byte trees (sdnr_tree_pack)."""
         _check(self._lib.sdnr_tree_pack(self._h, ctypes.c_void_p(parent_ptr),
@@ -407,6 +432,12 @@ class Context(object):
     def last_launches(self):
         n = ctypes.c_int32()
         _check(self._lib.sdnr_last_launches(self._h, ctypes.byref(n)))
+        return n.value
+
+    def last_sweeps(self):
+        """Bellman-Ford sweeps of the last APSP call (sdnr_last_sweeps)."""
+        n = ctypes.c_int32()
+        _check(self._lib.sdnr_last_sweeps(self._h, ctypes.byref(n)))
         return n.value
 
     def last_kernel_ms(self):

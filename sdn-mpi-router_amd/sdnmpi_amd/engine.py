@@ -186,6 +186,13 @@ def tree_port(w, layout, row_ptr, port, parent=None):
     return port[idx].to(x.dtype).masked_fill(none, -1)
 
 
+def _empty_rows(a, n):
+    """Uninitialised [n] + a.shape[1:] array of a's type (and device)."""
+    if _is_np(a):
+        return np.empty((n,) + tuple(a.shape[1:]), a.dtype)
+    return _torch().empty((n,) + tuple(a.shape[1:]), dtype=a.dtype, device=a.device)
+
+
 def _where(c, a, b):
     if _is_np(b):
         return np.where(c, a, b)
@@ -307,6 +314,31 @@ class RouteEngine(object):
                                        hop.data_ptr() if hop is not None else 0)
             self.ctx.synchronize()          # also raises on a tripped kernel watchdog
         return par, prt, hop
+
+    def empty_rows(self, n, V, dtypes):
+        """Uninitialised [n, V] device tensors of the named dtypes."""
+        return tuple(self._empty(n, V, getattr(self._torch, d)) for d in dtypes)
+
+    def dfs_tree_tables(self, export, srcs, layout, out=None):
+        """Default-route trees as 4-byte words of ``layout`` (PORT16 / SLOT)
+        plus depths (int16 holding u16 for V <= 65535, else int32), from the
+        DFS kernels directly (sdnr_dfs_tables_tree) -- into ``out`` (two
+        [S, V] tensors, e.g. pool rows) or new tensors."""
+        self.load(export)
+        t = self._torch
+        S, V = len(srcs), export.csr.V
+        if out is None:
+            out = self.empty_rows(S, V, ("int32", _hops_dtype(V)))
+        tree, dep = out
+        if S and V:
+            ts = self._ids(srcs)
+            self._ready()
+            self.ctx.dfs_tables_tree_device(
+                ts.data_ptr(), S, tree.data_ptr(), dep.data_ptr(),
+                _native.TREE_PORT16 if layout == PORT16 else _native.TREE_SLOT,
+                dep.element_size())
+            self.ctx.synchronize()          # also raises on a tripped kernel watchdog
+        return tree, dep
 
     def pack_trees(self, export, parent, port, layout):
         """int32 tables -> tree words (int32 tensor), sdnr_tree_pack."""
@@ -522,21 +554,38 @@ class _Pool(object):
                 a[_torch().as_tensor(idx, device=a.device)] = b
         self.free.extend(slots)
 
-    def add(self, verts, tabs):
-        """Store rows ``tabs`` ([n, V] each) for ``verts`` (room was made)."""
+    def add(self, verts, tabs=None, fill=None, like=None):
+        """Store rows for ``verts`` (room was made): either ``tabs`` ([n, V]
+        each, already computed) or ``fill(out)``, which computes them into
+        ``out`` -- views of the store itself when the slots taken are
+        contiguous (the kernels write their rows in place: no copy), else
+        fresh [n, V] arrays copied in afterwards.  ``like``: [0, V] arrays of
+        the tables' types (the first call allocates the store from them)."""
         if not verts:
             return
-        self._grow(len(self.row) + len(verts), tabs)
+        self._grow(len(self.row) + len(verts), tabs if tabs is not None else like)
         slots = [self.free.pop() for _ in verts]
         idx = np.asarray(slots, np.int64)
         contiguous = bool(np.all(np.diff(idx) == 1))
-        for a, t in zip(self.arrays, tabs):
-            if contiguous:
-                a[slots[0]:slots[0] + len(slots)] = t
-            elif _is_np(a):
-                a[idx] = t
-            else:
-                a.index_copy_(0, _torch().as_tensor(idx, device=a.device), t)
+        n = len(slots)
+        if tabs is None:
+            try:
+                if contiguous:
+                    fill(tuple(a[slots[0]:slots[0] + n] for a in self.arrays))
+                else:
+                    tabs = tuple(_empty_rows(a, n) for a in self.arrays)
+                    fill(tabs)
+            except BaseException:
+                self.free.extend(slots)            # nothing was stored
+                raise
+        if tabs is not None:
+            for a, t in zip(self.arrays, tabs):
+                if contiguous:
+                    a[slots[0]:slots[0] + n] = t
+                elif _is_np(a):
+                    a[idx] = t
+                else:
+                    a.index_copy_(0, _torch().as_tensor(idx, device=a.device), t)
         for v, s in zip(verts, slots):
             self.row[v] = s
             self.lru[v] = None
@@ -761,31 +810,37 @@ class TableCache(object):
             store.make_room(len(todo), set(wanted))
             for i in range(0, len(todo), COMPUTE_ROWS):
                 part = todo[i:i + COMPUTE_ROWS]
-                store.add(part, compute(np.asarray(part, np.int32)))
+                compute(store, part)
             self.rows_computed += len(todo)
         return store.tables()
 
-    def _dfs_compute(self, engine, srcs):
-        par, prt, hop = engine.dfs_tables(self.export, srcs)
+    def _dfs_compute(self, engine, store, part):
+        """Default-route rows of sources ``part`` into the pool.  Compact
+        layouts: the tree words and depths come straight from the DFS
+        kernels the bench times (sdnr_dfs_tables_tree), written into the
+        pool's own rows when the free slots are contiguous."""
+        srcs = np.asarray(part, np.int32)
         if self.layout == INT32:
-            return par, prt, hop
-        tree = engine.pack_trees(self.export, par, prt, self.layout)
-        if _is_np(hop):
-            return tree, hop.astype(_hops_dtype(self.V))
-        return tree, hop.to(getattr(_torch(), _hops_dtype(self.V)))
+            store.add(part, engine.dfs_tables(self.export, srcs))
+            return
+        like = engine.empty_rows(0, self.V, ("int32", _hops_dtype(self.V)))
+        store.add(part, fill=lambda out: engine.dfs_tree_tables(self.export, srcs, self.layout,
+                                                                out),
+                  like=like)
 
-    def _sp_compute(self, engine, dsts):
-        dist, nh, _ = engine.shortest_tables(self.export, dsts)
+    def _sp_compute(self, engine, store, part):
+        dist, nh, _ = engine.shortest_tables(self.export, np.asarray(part, np.int32))
         dt = _nh_dtype(self.V)
         if _is_np(dist):
-            return dist.view(np.int16), nh.astype(dt)
-        return dist, nh.to(getattr(_torch(), dt))
+            store.add(part, (dist.view(np.int16), nh.astype(dt)))
+        else:
+            store.add(part, (dist, nh.to(getattr(_torch(), dt))))
 
     def dfs_rows(self, engine, wanted, batch=()):
-        return self._rows(self.dfs, lambda s: self._dfs_compute(engine, s), wanted, batch)
+        return self._rows(self.dfs, lambda st, p: self._dfs_compute(engine, st, p), wanted, batch)
 
     def sp_rows(self, engine, wanted, batch=()):
-        return self._rows(self.sp, lambda d: self._sp_compute(engine, d), wanted, batch)
+        return self._rows(self.sp, lambda st, p: self._sp_compute(engine, st, p), wanted, batch)
 
 
 def tree_path(parent_row, s, d):

@@ -35,7 +35,7 @@ try:   # the reference takes OFPP_LOCAL from Ryu's OpenFlow 1.0 module (:5)
 except Exception:   # noqa: BLE001 - Ryu is not a dependency of the engine
     OFPP_LOCAL = 0xfffe
 
-__all__ = ["TopologyDB", "OFPP_LOCAL"]
+__all__ = ["TopologyDB", "OFPP_LOCAL", "sdn_mpi_mac"]
 
 _INF = 0xFFFF
 TABLE_SLICE_ENTRIES = 1 << 24     # table entries decoded per slice by route_tables()
@@ -448,6 +448,64 @@ class TopologyDB(object):
             hp_all[pos] = hp
         return off, ex.csr.dpids[np.asarray(sw_all, np.int64)], hp_all
 
+    def switch_fdb_entries(self, pairs):
+        """The flow entries of many (src_mac, dst_mac) pairs grouped by switch
+        -- what ``Router._add_flows_for_path`` records in ``SwitchFDB``
+        (reference ``sdnmpi/router.py:83-104``, ``util/switch_fdb.py:6-9``:
+        ``_dpid_to_fdb[dpid][(src, dst)] = out_port``) when every pair's route
+        is installed in order.  A (src, dst) key already recorded on a switch
+        keeps its first out_port, as the router's ``exists`` check does.
+
+        Returns ``(dpids, off, pair, out_port, last)`` numpy arrays: switch
+        ``dpids[k]`` holds the entries ``off[k]:off[k+1]``, entry j being
+        pair ``pair[j]`` (index into ``pairs``) leaving on ``out_port[j]``;
+        ``last[j]`` marks the pair's destination switch (where the router
+        adds the SetDlDst action for an MPI flow, :97-100).  Switches ascend
+        by dpid, entries keep pair order within a switch."""
+        pairs = list(pairs)
+        off, dp, pt = self.route_entries(pairs)
+        n = len(pairs)
+        lens = np.diff(off)
+        pid = np.repeat(np.arange(n, dtype=np.int64), lens)
+        last = np.zeros(int(off[-1]), bool)
+        ends = off[1:][lens > 0] - 1
+        last[ends] = True
+        # first occurrence of every (src, dst) key wins (SwitchFDB.exists)
+        keys = {}
+        first = np.fromiter((keys.setdefault(k, i) for i, k in enumerate(pairs)), np.int64, n)
+        keep = first[pid] == pid          # (routes are simple paths: one entry per switch)
+        pid, dp, pt, last = pid[keep], np.asarray(dp)[keep], np.asarray(pt)[keep], last[keep]
+        order = np.lexsort((np.arange(pid.shape[0]), dp))           # by dpid, stable
+        dp, pid, pt, last = dp[order], pid[order], pt[order], last[order]
+        if dp.shape[0]:
+            newsw = np.ones(dp.shape[0], bool)
+            newsw[1:] = dp[1:] != dp[:-1]
+            starts = np.nonzero(newsw)[0]
+            dpids = dp[starts]
+            soff = np.append(starts, dp.shape[0]).astype(np.int64)
+        else:
+            dpids = np.zeros(0, np.int64)
+            soff = np.zeros(1, np.int64)
+        return dpids.astype(np.int64), soff, pid, pt.astype(np.int32), last
+
+    def mpi_flow_entries(self, rank_to_mac, coll_type=0):
+        """The SDN-MPI flows of every ordered rank pair of a job, grouped by
+        switch: for ranks i != j (``rank_to_mac``: ProcessManager's
+        RankAllocationDB map, reference ``process.py:107-110``) the router
+        installs, per switch of ``find_route(mac_i, mac_j)``, a flow matching
+        (src ``mac_i``, dst the virtual address ``sdn_mpi_mac(coll_type, i,
+        j)``) whose last hop rewrites the destination to ``mac_j``
+        (``router.py:166-200``).  Returns ``(dpids, off, src_rank, dst_rank,
+        out_port, last)`` as :meth:`switch_fdb_entries` lays them out."""
+        ranks = sorted(rank_to_mac)
+        src_r = [a for a in ranks for b in ranks if a != b]
+        dst_r = [b for a in ranks for b in ranks if a != b]
+        pairs = [(rank_to_mac[a], rank_to_mac[b]) for a, b in zip(src_r, dst_r)]
+        dpids, off, pid, pt, last = self.switch_fdb_entries(pairs)
+        sr = np.asarray(src_r, np.int64)[pid] if pid.size else np.zeros(0, np.int64)
+        dr = np.asarray(dst_r, np.int64)[pid] if pid.size else np.zeros(0, np.int64)
+        return dpids, off, sr, dr, pt, last
+
     def find_routes(self, pairs, multiple=False):
         """find_route over many (src_mac, dst_mac) pairs; tables are computed
         once for all of them, and the default-route fdbs of large batches are
@@ -470,6 +528,16 @@ class TopologyDB(object):
             if len(want) < self._cache.dfs.cap():
                 self._cache.dfs_rows(self.engine, sorted(want), self._host_vertices(ex))
         return [self.find_route(a, b, multiple) for a, b in pairs]
+
+
+def sdn_mpi_mac(coll_type, src_rank, dst_rank):
+    """The virtual destination MAC of an SDN-MPI message, as the router
+    decodes it (reference ``sdnmpi/router.py:163-178``): locally administered
+    bit 0x02 and the collective type << 2 in byte 0, the source and
+    destination ranks as little-endian int16 in bytes 2-3 and 4-5."""
+    b = [((int(coll_type) << 2) | 0x02) & 0xFF, 0,
+         src_rank & 0xFF, (src_rank >> 8) & 0xFF, dst_rank & 0xFF, (dst_rank >> 8) & 0xFF]
+    return ":".join("%02x" % x for x in b)
 
 
 def _same_graph(a, b):

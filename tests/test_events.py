@@ -167,6 +167,13 @@ class _TimedEngine(_FakeEngine):
         finally:
             self.spent += time.perf_counter() - t
 
+    def dfs_tree_tables(self, *a, **k):
+        t = time.perf_counter()
+        try:
+            return super(_TimedEngine, self).dfs_tree_tables(*a, **k)
+        finally:
+            self.spent += time.perf_counter() - t
+
 
 def test_jellyfish_events_are_o_change():
     fabric = T.jellyfish(100000, 16, seed=1)

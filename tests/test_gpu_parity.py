@@ -134,6 +134,126 @@ def test_dfs_slots_small(ctx, monkeypatch, name, strategy):
     np.testing.assert_array_equal(t, to)
 
 
+def _check_tree_depth(csr, srcs, tree, depth, layout, depth_bytes):
+    po, to, ho = O.dfs_tables(csr, srcs, nthreads=NTHREADS)
+    want = _pack(po, to) if layout == _native.TREE_PORT16 else _expected_slots(csr, po)
+    np.testing.assert_array_equal(tree, want)
+    if depth_bytes == 2:
+        np.testing.assert_array_equal(depth, ho.astype(np.uint16))   # -1 -> 0xFFFF
+    else:
+        np.testing.assert_array_equal(depth, ho)
+
+
+@pytest.mark.parametrize("strategy", ["auto", "async", "lds", "global", "global-nosplit"])
+@pytest.mark.parametrize("layout", ["port16", "slot"])
+@pytest.mark.parametrize("depth_bytes", [2, 4])
+@pytest.mark.parametrize("name", ["mock", "fat_tree_k8", "dragonfly_a4_h2_p2", "random_V40",
+                                  "jellyfish_n60_r5", "torus_5x3x2"])
+def test_dfs_tree_depth_small(ctx, monkeypatch, name, layout, depth_bytes, strategy):
+    """sdnr_dfs_tables_tree: 4-byte tree words + depths straight from every
+    DFS strategy (the drop-in's pool rows), bit-exact vs the oracle."""
+    _strategy(monkeypatch, None if strategy == "auto" else strategy)
+    csr = G.Golden(name).fabric().csr()
+    srcs = np.arange(csr.V, dtype=np.int32)
+    ctx.upload(csr)
+    lay = _native.TREE_PORT16 if layout == "port16" else _native.TREE_SLOT
+    tree, depth = ctx.dfs_tables_tree(srcs, lay, depth_bytes)
+    _check_tree_depth(csr, srcs, tree, depth, lay, depth_bytes)
+
+
+@pytest.mark.parametrize("nsrc", [1, 144, 1152])
+def test_dfs_tree_depth_k48(ctx, nsrc):
+    """The drop-in's fill on k=48 runs the benched async kernel with hop
+    counts (u16 depth plane), no int32 intermediate."""
+    fabric = T.fat_tree(48)
+    csr = fabric.csr()
+    srcs = np.unique(fabric.host_table()[0]).astype(np.int32)[:nsrc]
+    ctx.upload(csr)
+    tree, depth = ctx.dfs_tables_tree(srcs, _native.TREE_PORT16, 2)
+    assert ctx.last_kernel().startswith("dfs_async_kernel<") and \
+        ctx.last_kernel().endswith(",packed,hops>")
+    _check_tree_depth(csr, srcs, tree, depth, _native.TREE_PORT16, 2)
+
+
+@pytest.mark.parametrize("waves", ["auto", "2", "3", "8"])
+@pytest.mark.parametrize("name", ["mock", "fat_tree_k4", "fat_tree_k8", "dragonfly_a4_h2_p2",
+                                  "random_V40", "random_V12", "random_V9", "jellyfish_n60_r5",
+                                  "torus_5x3x2", "torus_4x4x4", "random_V60_dense"])
+def test_dfs_bits_small(ctx, monkeypatch, name, waves):
+    """dfs_bits_kernel (visited set in registers, bitmap rows, frame log):
+    int32 tables with hops, packed trees, tree + u16 depth, all bit-exact vs
+    the oracle on every vertex as a source -- directed graphs, sparse dpids,
+    isolated switches included."""
+    _strategy(monkeypatch, "bits")
+    if waves != "auto":
+        monkeypatch.setenv("SDNROUTE_DFS_BITS_WAVES", waves)
+    csr = G.Golden(name).fabric().csr()
+    srcs = np.concatenate([np.arange(csr.V), [-1, csr.V + 3]]).astype(np.int32)
+    ctx.upload(csr)
+    p, t, h = ctx.dfs_tables(srcs)
+    assert ctx.last_kernel() == "dfs_bits_kernel<hops>"
+    po, to, ho = O.dfs_tables(csr, srcs, nthreads=NTHREADS)
+    np.testing.assert_array_equal(p, po)
+    np.testing.assert_array_equal(t, to)
+    np.testing.assert_array_equal(h, ho)
+    if csr.E and int(csr.port.max()) < 0xFFFF:
+        tree = ctx.dfs_tables_packed(srcs)
+        assert ctx.last_kernel() == "dfs_bits_kernel<packed>"
+        np.testing.assert_array_equal(tree, _pack(po, to))
+        tree, depth = ctx.dfs_tables_tree(srcs, _native.TREE_PORT16, 2)
+        assert ctx.last_kernel() == "dfs_bits_kernel<packed,hops>"
+        np.testing.assert_array_equal(tree, _pack(po, to))
+        np.testing.assert_array_equal(depth, ho.astype(np.uint16))
+
+
+@pytest.mark.parametrize("name", ["fat_tree_k48", "dragonfly_a16_h8_p8"])
+@pytest.mark.parametrize("nsrc", [1, 144, 0])
+def test_dfs_bits_fullsize(ctx, monkeypatch, name, nsrc):
+    """The bits kernel on the BASELINE small-V fabrics: every host source
+    (k=48: 1,152; dragonfly: 2,064), or the first 1 / 144 (one GPU's share
+    at N=8), packed trees bit-exact vs the oracle."""
+    _strategy(monkeypatch, "bits")
+    fabric = T.fat_tree(48) if name == "fat_tree_k48" else T.dragonfly(16, 8, 8)
+    csr = fabric.csr()
+    srcs = np.unique(fabric.host_table()[0]).astype(np.int32)
+    if nsrc:
+        srcs = srcs[:nsrc]
+    ctx.upload(csr)
+    tree = ctx.dfs_tables_packed(srcs)
+    assert ctx.last_kernel() == "dfs_bits_kernel<packed>"
+    po, to, _ = O.dfs_tables(csr, srcs, with_hops=False, nthreads=NTHREADS)
+    np.testing.assert_array_equal(tree, _pack(po, to))
+
+
+@pytest.mark.parametrize("V", [4000, 4096])
+def test_dfs_bits_log_spill(ctx, monkeypatch, V):
+    """Graphs whose frame log, frame headers and stack outgrow their LDS
+    parts (768 / 384 / 192): a long path with branches (deep stack, many
+    frames) -- the spill to global memory stays bit-exact."""
+    _strategy(monkeypatch, "bits")
+    rng = np.random.default_rng(V)
+    src, dst = [], []
+    for u in range(V - 1):                       # a chain 0-1-2-..., both ways
+        src += [u, u + 1]
+        dst += [u + 1, u]
+    for _ in range(V // 2):                      # plus random chords
+        a, b = (int(x) for x in rng.integers(0, V, 2))
+        if a != b:
+            src += [a, b]
+            dst += [b, a]
+    from sdnmpi_amd.topologies import build_csr
+    e = np.unique(np.stack([src, dst], 1), axis=0)
+    csr = build_csr(e[:, 0] + 1, e[:, 1] + 1, np.arange(e.shape[0]) % 60 + 1)
+    srcs = np.array([0, 1, V // 2, V - 1], np.int32)
+    ctx.upload(csr)
+    p, t, h = ctx.dfs_tables(srcs)
+    assert ctx.last_kernel() == "dfs_bits_kernel<hops>"
+    po, to, ho = O.dfs_tables(csr, srcs, nthreads=NTHREADS)
+    np.testing.assert_array_equal(p, po)
+    np.testing.assert_array_equal(t, to)
+    np.testing.assert_array_equal(h, ho)
+
+
 @pytest.mark.parametrize("strategy", ["runs", "async"])
 def test_dfs_packed_fullsize_k48(ctx, monkeypatch, strategy):
     _strategy(monkeypatch, strategy)
@@ -510,12 +630,15 @@ def test_shortest_global_path_torus(ctx):
     np.testing.assert_array_equal(nhp, nhpo)
 
 
-@pytest.mark.parametrize("algo", ["squaring", "sq128", "fw"])
+@pytest.mark.parametrize("algo", ["squaring", "squaring-norelax", "sq128", "fw"])
 @pytest.mark.parametrize("name", ["mock", "fat_tree_k8", "dragonfly_a4_h2_p2",
                                   "random_V60_dense", "torus_5x3x2", "random_V40", "random_V9"])
 def test_apsp_small(ctx, monkeypatch, name, algo):
-    if algo != "squaring":
+    if algo == "squaring-norelax":               # squaring passes only, no sweeps
+        monkeypatch.setenv("SDNROUTE_APSP_RELAX", "0")
+    elif algo != "squaring":
         monkeypatch.setenv("SDNROUTE_APSP", algo)
+        monkeypatch.setenv("SDNROUTE_APSP_RELAX", "0")
     csr = G.Golden(name).fabric().csr()
     ctx.upload(csr)
     np.testing.assert_array_equal(ctx.apsp(), O.apsp(csr))
@@ -553,32 +676,48 @@ def test_shortest_unknown_destination_rows_device(ctx):
     assert (nh.cpu().numpy()[[0, 2]] == -1).all()
 
 
-@pytest.mark.parametrize("tiles", ["64", "sq128"])
+@pytest.mark.parametrize("tiles", ["64", "sq128", "64-norelax"])
 def test_apsp_fullsize_k48(ctx, monkeypatch, tiles):
+    """k=48 (diameter 4): Bellman-Ford sweeps reach the fixpoint within the
+    cap, no squaring pass at all; squaring alone takes 3 passes."""
     if tiles == "sq128":
         monkeypatch.setenv("SDNROUTE_APSP", "sq128")
+    if tiles != "64":
+        monkeypatch.setenv("SDNROUTE_APSP_RELAX", "0")
     csr = T.fat_tree(48).csr()
     ctx.upload(csr)
     D = ctx.apsp()
-    assert ctx.last_kernel() == ("minplus_square_kernel" if tiles == "sq128"
-                                 else "minplus_square64_kernel")
+    if tiles == "64":
+        assert ctx.last_kernel() == "apsp_relax8_kernel"
+        assert ctx.last_launches() == 0 and 2 <= ctx.last_sweeps() <= 5
+    else:
+        assert ctx.last_kernel() == ("minplus_square_kernel" if tiles == "sq128"
+                                     else "minplus_square64_kernel")
+        assert ctx.last_launches() == 3 and ctx.last_sweeps() == 0
     np.testing.assert_array_equal(D, O.apsp(csr))
 
 
-@pytest.mark.parametrize("tiles", ["64", "sq128"])
+@pytest.mark.parametrize("tiles", ["64", "sq128", "64-norelax"])
 def test_apsp_long_paths_torus(ctx, monkeypatch, tiles):
-    """A high-diameter graph (ring-like torus 40x3x1): many squarings."""
+    """A high-diameter graph (ring-like torus 40x3x1, diameter 21): squaring
+    alone takes many passes; with sweeps, the cap (5 here) runs out and
+    squaring passes alternate with sweeps."""
     if tiles == "sq128":
         monkeypatch.setenv("SDNROUTE_APSP", "sq128")
+    if tiles != "64":
+        monkeypatch.setenv("SDNROUTE_APSP_RELAX", "0")
     csr = T.torus3d(40, 3, 1).csr()
     ctx.upload(csr)
     np.testing.assert_array_equal(ctx.apsp(), O.apsp(csr))
+    if tiles == "64":
+        assert ctx.last_launches() >= 1 and ctx.last_sweeps() >= 5
 
 
 @pytest.mark.parametrize("tiles", ["64", "sq128"])
 def test_apsp_dragonfly(ctx, monkeypatch, tiles):
     if tiles == "sq128":
         monkeypatch.setenv("SDNROUTE_APSP", "sq128")
+        monkeypatch.setenv("SDNROUTE_APSP_RELAX", "0")
     csr = T.dragonfly(16, 8, 8).csr()
     ctx.upload(csr)
     np.testing.assert_array_equal(ctx.apsp(), O.apsp(csr))

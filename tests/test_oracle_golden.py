@@ -68,7 +68,24 @@ def test_per_pair_oracle_matches_reference(name):
     macs = fabric.host_macs()
     step = max(1, len(g) // 1500)
     for i in range(0, len(g), step):
-        assert O.find_route_pair(db, macs[g.pair_src[i]], macs[g.pair_dst[i]]) == g.fdb(i)
+        a, b = macs[g.pair_src[i]], macs[g.pair_dst[i]]
+        assert O.find_route_pair(db, a, b) == g.fdb(i)
+        # the path-copying form (the reference's own search shape, timed as
+        # bench.py's cpu_reference_path)
+        assert O.find_route_pair(db, a, b, copying=True) == g.fdb(i)
+
+
+@pytest.mark.parametrize("name", ["fat_tree_k48_sample", "dragonfly_a16_h8_p8_sample"])
+def test_per_pair_copying_oracle_matches_reference_fullsize(name):
+    """The path-copying restatement on the reference's own sampled pairs of
+    the full-size fabrics (the bench's CPU reference-path workload)."""
+    g = G.Golden(name)
+    fabric = g.fabric()
+    db = fabric.populate(_DictDB())
+    macs = fabric.host_macs()
+    for i in range(0, len(g), max(1, len(g) // 40)):
+        a, b = macs[g.pair_src[i]], macs[g.pair_dst[i]]
+        assert O.find_route_pair(db, a, b, copying=True) == g.fdb(i)
 
 
 @pytest.mark.parametrize("name", G.MULTI)
@@ -150,6 +167,7 @@ def test_scenarios_per_pair_oracle():
                 got = O.find_routes_all_shortest(db, a, b)
             else:
                 got = O.find_route_pair(db, a, b)
+                assert O.find_route_pair(db, a, b, copying=True) == got
             assert got == G.as_tuples(want), (sc["name"], a, b, multiple)
         for a, b, exc in sc.get("raises", []):
             with pytest.raises(Exception) as ei:

@@ -161,6 +161,22 @@ class _FakeEngine(object):
         from sdnmpi_amd.engine import pack_host_tree
         return pack_host_tree(parent, port, export.csr, layout)
 
+    def empty_rows(self, n, V, dtypes):
+        return tuple(np.empty((n, V), d) for d in dtypes)
+
+    def dfs_tree_tables(self, export, srcs, layout, out=None):
+        # oracle trees packed on the host (test double of sdnr_dfs_tables_tree)
+        from sdnmpi_amd.engine import pack_host_tree
+        self.calls.append(("dfs", export.key, tuple(int(x) for x in srcs)))
+        par, prt, hop = self.O.dfs_tables(export.csr, srcs)
+        tree = pack_host_tree(par, prt, export.csr, layout)
+        dep = hop.astype(np.int16 if export.csr.V <= 0xFFFF else np.int32)
+        if out is None:
+            return tree, dep
+        out[0][...] = tree
+        out[1][...] = dep
+        return out
+
     def ecmp(self, export, dist, rows, srcs):
         # host walk of the shortest-path DAG (test double only)
         from sdnmpi_amd.engine import shortest_paths_lex
@@ -304,7 +320,7 @@ def test_route_entries_batched_fake_engine():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("walk", ["auto", "serial", "int32", "p4", "p8"])
+@pytest.mark.parametrize("walk", ["auto", "jump16", "serial", "int32", "p4", "p8"])
 @pytest.mark.parametrize("name", ["mock", "fat_tree_k8", "dragonfly_a4_h2_p2", "random_V40",
                                   "torus_5x3x2"])
 def test_route_entries_match_reference(monkeypatch, name, walk):
@@ -313,6 +329,8 @@ def test_route_entries_match_reference(monkeypatch, name, walk):
     from oracle import oracle as O
     if walk == "serial":
         monkeypatch.setenv("SDNROUTE_ROUTE_WALK", walk)
+    elif walk == "jump16":                       # packed per-entry jump walks
+        monkeypatch.setenv("SDNROUTE_ROUTE_SEG", "0")
     elif walk != "auto":                         # int32-table jump kernels
         monkeypatch.setenv("SDNROUTE_ROUTE_PACKED", "0")
         if walk != "int32":
@@ -346,7 +364,46 @@ def test_route_entries_k48_many_pairs(monkeypatch):
     assert db.engine.ctx.last_kernel() == "route_walk_kernel"
     monkeypatch.delenv("SDNROUTE_ROUTE_WALK")
     o1, d1, p1 = db.route_entries(pairs)
+    assert db.engine.ctx.last_kernel() == "route_seg_packed_kernel<1024>"
+    np.testing.assert_array_equal(o0, o1)
+    np.testing.assert_array_equal(d0, d1)
+    np.testing.assert_array_equal(p0, p1)
+    monkeypatch.setenv("SDNROUTE_ROUTE_SEG", "0")
+    o2, d2, p2 = db.route_entries(pairs)
     assert db.engine.ctx.last_kernel() == "route_jump_packed_kernel<16>"
+    np.testing.assert_array_equal(o0, o2)
+    np.testing.assert_array_equal(d0, d2)
+    np.testing.assert_array_equal(p0, p2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fab", ["fat_tree:48", "torus:16,16,16"])
+def test_route_entries_runs_and_long_paths(monkeypatch, fab):
+    """The output-centric expansion (route_seg_packed_kernel): pairs in runs
+    of one (source switch, destination switch) -- all hosts of a few switch
+    pairs, in the all-pairs order -- mixed with scattered and same-switch
+    pairs; on the torus the DFS routes (hundreds to thousands of entries)
+    overflow the per-wave buffer and take the direct walk.  Entries equal the
+    one-lane-per-pair serial walk's."""
+    from sdnmpi_amd import topologies as T
+    fabric = T.by_name(fab)
+    db = fabric.populate(TopologyDB())
+    macs = fabric.host_macs()
+    rng = np.random.default_rng(11)
+    sw = fabric.host_table()[0]
+    order = np.argsort(sw, kind="stable")
+    ms = [macs[int(i)] for i in order]          # hosts grouped by switch
+    block = ms[: 3 * 24] if fab.startswith("fat") else ms[:40]
+    pairs = [(a, b) for a in block for b in block]
+    pairs += [(macs[int(x)], macs[int(y)]) for x, y in rng.integers(0, len(macs), (3000, 2))]
+    pairs += [(macs[5], macs[5])] * 70
+    monkeypatch.setenv("SDNROUTE_ROUTE_WALK", "serial")
+    o0, d0, p0 = db.route_entries(pairs)
+    monkeypatch.delenv("SDNROUTE_ROUTE_WALK")
+    o1, d1, p1 = db.route_entries(pairs)
+    assert db.engine.ctx.last_kernel() == "route_seg_packed_kernel<1024>"
+    if not fab.startswith("fat"):
+        assert int(np.diff(o0).max()) > 1024     # some pairs take the direct walk
     np.testing.assert_array_equal(o0, o1)
     np.testing.assert_array_equal(d0, d1)
     np.testing.assert_array_equal(p0, p1)
@@ -527,3 +584,80 @@ def test_unsigned_64bit_dpids():
         for b in macs:
             assert db.find_route(a, b) == O.find_route_pair(db, a, b)
             assert db.find_route(a, b, True) == O.find_routes_all_shortest(db, a, b)
+
+
+def _replay_switch_fdb(db, pairs, keys=None):
+    """Reference-shaped replay of Router._add_flows_for_path into a
+    SwitchFDB-like dict (sdnmpi/router.py:83-104, util/switch_fdb.py:6-9):
+    fdb = find_route(src, dst) per pair, one (dpid, (src, dst)) -> out_port
+    per hop, an existing key kept."""
+    from oracle import oracle as O
+    out = {}
+    for i, (a, b) in enumerate(pairs):
+        key = keys[i] if keys else (a, b)
+        for dpid, port in O.find_route_pair(db, a, b):
+            sw = out.setdefault(dpid, {})
+            if key not in sw:
+                sw[key] = port
+    return out
+
+
+def _grouped_to_dict(dpids, off, keys, port):
+    out = {}
+    for k in range(dpids.shape[0]):
+        sw = out.setdefault(int(dpids[k]), {})
+        for j in range(int(off[k]), int(off[k + 1])):
+            sw[keys[j]] = int(port[j])
+    return out
+
+
+def _switch_fdb_check(db, fabric, rng):
+    macs = fabric.host_macs()
+    pairs = [(macs[int(a)], macs[int(b)]) for a, b in rng.integers(0, len(macs), (300, 2))]
+    pairs += pairs[:20] + [(macs[0], "02:00:00:00:00:77")]      # repeated keys, unknown host
+    dpids, off, pid, port, last = db.switch_fdb_entries(pairs)
+    assert np.all(np.diff(dpids) > 0)
+    got = _grouped_to_dict(dpids, off, [pairs[int(i)] for i in pid], port)
+    assert got == _replay_switch_fdb(db, pairs)
+    # the last flag marks each pair's destination switch
+    for j in np.nonzero(last)[0][:50]:
+        a, b = pairs[int(pid[j])]
+        k = int(np.searchsorted(off, j, side="right") - 1)
+        assert int(dpids[k]) == db.hosts[b].port.dpid
+    # the MPI rank set: every ordered rank pair, keyed by (src rank, dst rank)
+    ranks = {r: macs[int(h)] for r, h in enumerate(rng.choice(len(macs), 12, replace=False))}
+    dpids, off, sr, dr, port, last = db.mpi_flow_entries(ranks, coll_type=3)
+    rp = [(a, b) for a in sorted(ranks) for b in sorted(ranks) if a != b]
+    want = _replay_switch_fdb(db, [(ranks[a], ranks[b]) for a, b in rp], keys=rp)
+    got = _grouped_to_dict(dpids, off, list(zip(sr.tolist(), dr.tolist())), port)
+    assert got == want
+
+
+def test_switch_fdb_entries_fake_engine():
+    from sdnmpi_amd import topologies as T
+    for fabric in (T.fat_tree(4), T.fat_tree(8)):
+        db = fabric.populate(TopologyDB())
+        db._engine = _FakeEngine()
+        _switch_fdb_check(db, fabric, np.random.default_rng(3))
+
+
+def test_sdn_mpi_mac_matches_router_decoding():
+    """sdn_mpi_mac round-trips through the router's decoding (reference
+    sdnmpi/router.py:163-178): locally administered bit, collective type,
+    little-endian int16 ranks."""
+    import struct
+    from sdnmpi_amd.util.topology_db import sdn_mpi_mac
+    for coll, a, b in [(0, 0, 1), (3, 17, 4095), (63, 32767, 0), (5, 300, 256)]:
+        raw = bytes(int(x, 16) for x in sdn_mpi_mac(coll, a, b).split(":"))
+        assert raw[0] & 0x02
+        assert raw[0] >> 2 == coll
+        assert struct.unpack("<h", raw[2:4])[0] == a
+        assert struct.unpack("<h", raw[4:6])[0] == b
+
+
+@pytest.mark.gpu
+def test_switch_fdb_entries_gpu():
+    from sdnmpi_amd import topologies as T
+    for fabric in (T.fat_tree(8), T.fat_tree(48)):
+        db = fabric.populate(TopologyDB())
+        _switch_fdb_check(db, fabric, np.random.default_rng(4))
