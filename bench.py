@@ -306,6 +306,17 @@ def materialised_flows(ctx, dev, stream, csr, fabric, srcs, chunk=1 << 24):
         a, b = idx // H, idx % H
         reqs.append((row_of_host[a].contiguous(), sw_of_host[b].contiguous(),
                      port_of_host[b].contiguous()))
+    # untimed: one chunk through the whole output buffer first (first-touch
+    # page mapping of the 2 x chunk x max_len words happens here, not in the
+    # timed loop)
+    rows, dsts, last = reqs[0]
+    ctx.route_offsets_device(hop.data_ptr(), rows.data_ptr(), dsts.data_ptr(), rows.shape[0],
+                             off.data_ptr(), nrows=S)
+    ctx.expand_routes_device(par.data_ptr(), prt.data_ptr(), S, rows.data_ptr(), dsts.data_ptr(),
+                             last.data_ptr(), rows.shape[0], off.data_ptr(), sw.data_ptr(),
+                             hpo.data_ptr())
+    sw.fill_(0)
+    hpo.fill_(0)
     torch.cuda.synchronize(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     entries = torch.zeros((), dtype=torch.int64, device=dev)

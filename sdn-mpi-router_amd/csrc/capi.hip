@@ -66,12 +66,17 @@ int sdnr_reserve(void **buf, size_t *cur, size_t need)
     return SDNR_OK;
 }
 
-int sdnr_fetch_ints(sdnr_ctx *ctx, const int *d_src, int n, int *out)
+int sdnr_fetch_ints_begin(sdnr_ctx *ctx, const int *d_src, int n)
 {
     if (n < 1 || n > 4) return sdnr_fail(SDNR_ERR_INVAL, "sdnr_fetch_ints: %d words", n);
     SDNR_HIP(hipMemcpyAsync(ctx->h_flag, d_src, (size_t)n * sizeof(int), hipMemcpyDeviceToHost,
                             ctx->stream));
     SDNR_HIP(hipEventRecord(ctx->ev_flag, ctx->stream));
+    return SDNR_OK;
+}
+
+int sdnr_fetch_ints_end(sdnr_ctx *ctx, int n, int *out)
+{
     for (;;) {
         const hipError_t e = hipEventQuery(ctx->ev_flag);
         if (e == hipSuccess) break;
@@ -79,6 +84,12 @@ int sdnr_fetch_ints(sdnr_ctx *ctx, const int *d_src, int n, int *out)
     }
     for (int i = 0; i < n; ++i) out[i] = reinterpret_cast<volatile int *>(ctx->h_flag)[i];
     return SDNR_OK;
+}
+
+int sdnr_fetch_ints(sdnr_ctx *ctx, const int *d_src, int n, int *out)
+{
+    const int rc = sdnr_fetch_ints_begin(ctx, d_src, n);
+    return rc ? rc : sdnr_fetch_ints_end(ctx, n, out);
 }
 
 static void free_graph(sdnr_ctx *c)

@@ -126,6 +126,10 @@ int sdnr_check_watchdog(sdnr_ctx *ctx);   // after a stream sync
 // busy spin on an event: a level loop's termination check costs a few
 // microseconds instead of a blocking stream synchronize's wake-up
 int sdnr_fetch_ints(sdnr_ctx *ctx, const int *d_src, int n, int *out);
+// the same in two halves: the copy + event go on the stream, more work may
+// follow them, then the host waits for the event (the words as of then)
+int sdnr_fetch_ints_begin(sdnr_ctx *ctx, const int *d_src, int n);
+int sdnr_fetch_ints_end(sdnr_ctx *ctx, int n, int *out);
 
 #define SDNR_HIP(call)                                           \
     do {                                                         \

@@ -48,11 +48,21 @@ namespace {
 constexpr int kBitsEmax = 768;           // log entries in LDS
 constexpr int kBitsFmax = 384;           // frame headers in LDS
 constexpr int kBitsDmax = 192;           // stack entries in LDS
-constexpr int kBitsG = 16;               // children per worker step
+constexpr int kBitsG = 8;                // children per worker step
+constexpr int kBitsK = 4;                // candidates tested together
 constexpr unsigned kBitsSpin = 1u << 22;
 constexpr int kBitsFlagPrio = 1;         // search wave at raised issue priority
 constexpr int kBitsFlagHops16 = 32;      // hop counts as u16 (0xFFFF unreached)
 constexpr unsigned kBitsDummyInit = 0x40000000u;
+
+#ifdef SDNR_STAMPS
+// diagnostic build only (tools/build_stamps.sh): per-phase cycle and event
+// counts of the search wave, summed over sources (sdnr_debug_bits_stamps)
+__device__ unsigned long long g_bits_stamp[16];
+#define BITS_STAMP(i, v) atomicAdd(&g_bits_stamp[i], (unsigned long long)(v))
+#else
+#define BITS_STAMP(i, v) do { (void)(v); } while (0)
+#endif
 
 __device__ __forceinline__ uint64_t read_lane64(uint64_t x, int l)
 {
@@ -177,12 +187,27 @@ __global__ __launch_bounds__(NW * 64) void dfs_bits_kernel(
             int Lid = -1;
             uint64_t M = 0;
             int u = s, du = 0;
-            int pfu = s;
-            uint64_t pfrow = adjb[(size_t)s * 64 + lane];
+            int pfu = -1;
+            uint64_t pfrow = 0ull;
+            uint64_t rb = adjb[(size_t)s * 64 + lane];   // row of the vertex to explore
             bool spilled = false;
+#ifdef SDNR_STAMPS
+            unsigned long long z0 = __builtin_readcyclecounter(), za, zb, z_ex = 0, z_sel = 0;
+            unsigned long long n_ex = 0, n_false = 0, n_ret = 0, n_miss = 0;
+#endif
+            // frame & NL below the cursor x: drop x and every bit above it
+            auto below = [&](uint64_t &mm, int x) {
+                const int xl = x >> 6;
+                if (Lid > xl) mm = 0ull;
+                else if (Lid == xl) mm &= (1ull << (x & 63)) - 1ull;
+            };
             for (;;) {
-                // ---- explore u
-                const uint64_t rb = u == pfu ? pfrow : adjb[(size_t)u * 64 + lane];
+                // ---- explore u (its row in rb, its fresh children non-empty
+                // unless u is the source)
+#ifdef SDNR_STAMPS
+                za = __builtin_readcyclecounter();
+                n_ex++;
+#endif
                 const uint64_t fresh = rb & ~vis;
                 const uint64_t fm = __ballot(fresh != 0ull);
                 if (fm) {
@@ -224,31 +249,79 @@ __global__ __launch_bounds__(NW * 64) void dfs_bits_kernel(
                     pfu = c1;
                     pfrow = adjb[(size_t)c1 * 64 + lane];
                 }
-                // ---- the next candidate: highest bit of frame & NL
+#ifdef SDNR_STAMPS
+                else {
+                    n_false++;
+                }
+                zb = __builtin_readcyclecounter();
+                z_ex += zb - za;
+#endif
+                // ---- the next vertex to explore: among the highest bits of
+                // frame & NL (NL may be stale-set: a candidate may be a leaf
+                // after all), up to K at a time are tested exactly -- their
+                // rows loaded together, the first with a fresh child wins
                 bool done = false;
                 for (;;) {
                     const uint64_t nl = Lid >= 0 ? __hip_atomic_load(&NL[Lid], __ATOMIC_RELAXED,
                                                                       __HIP_MEMORY_SCOPE_WORKGROUP)
                                                  : 0ull;
-                    const uint64_t cand = M & nl;
-                    const uint64_t cm = __ballot(cand != 0ull);
-                    if (cm) {
-                        const int h = highest_lane(cm);
-                        const int b = 63 - __clzll(read_lane64(cand, h));
-                        const int L = read_lane(Lid, h);
-                        // nu and every bit above it leave the frame (the
-                        // ones above are leaf pops)
-                        if (lane > h) M = 0ull;
-                        else if (lane == h) M &= (1ull << b) - 1ull;
-                        u = 64 * L + b;
-                        du = fdep + 1;
-                        break;
+                    uint64_t cand = M & nl;
+                    int cv[kBitsK];
+                    int nc = 0;
+#pragma unroll
+                    for (int q = 0; q < kBitsK; ++q) {
+                        cv[q] = -1;
+                        const uint64_t cm = __ballot(cand != 0ull);
+                        if (cm) {
+                            const int h = highest_lane(cm);
+                            const int b = 63 - __clzll(read_lane64(cand, h));
+                            cv[q] = 64 * read_lane(Lid, h) + b;
+                            if (lane == h) cand &= ~(1ull << b);
+                            ++nc;
+                        }
+                    }
+                    if (nc) {
+                        uint64_t rk[kBitsK];
+#pragma unroll
+                        for (int q = 0; q < kBitsK; ++q)
+                            if (q < nc) rk[q] = cv[q] == pfu ? pfrow : adjb[(size_t)cv[q] * 64 + lane];
+                        int pick = -1;
+#pragma unroll
+                        for (int q = 0; q < kBitsK; ++q) {
+                            if (pick < 0 && q < nc) {
+                                if (__ballot((rk[q] & ~vis) != 0ull)) {
+                                    pick = q;
+                                    rb = rk[q];
+                                }
+                            }
+                        }
+#ifdef SDNR_STAMPS
+                        n_false += pick < 0 ? nc : pick;
+                        if (cv[0] != pfu) n_miss++;
+#endif
+                        if (pick >= 0) {
+                            // the picked vertex and every bit above it leave
+                            // the frame (the ones above are leaf pops)
+                            int x = cv[0];
+#pragma unroll
+                            for (int q = 0; q < kBitsK; ++q)
+                                if (q == pick) x = cv[q];
+                            below(M, x);
+                            u = x;
+                            du = fdep + 1;
+                            break;
+                        }
+                        below(M, cv[nc - 1]);    // all leaves: popped
+                        continue;
                     }
                     // frame exhausted: back to the saved one below
                     if (sp == 0) {
                         done = true;
                         break;
                     }
+#ifdef SDNR_STAMPS
+                    n_ret++;
+#endif
                     --sp;
                     // the spill area is reused across sources: this wave's own
                     // stores must be done and no stale line read (rare path)
@@ -274,26 +347,35 @@ __global__ __launch_bounds__(NW * 64) void dfs_bits_kernel(
                         Lid = (int)(t & 63u);
                     }
                     fdep = (int)(read_lane((int)t, 0) >> 18);
-                    const int cl = cur >> 6;
-                    if (Lid > cl) M = 0ull;
-                    else if (Lid == cl) M &= (1ull << (cur & 63)) - 1ull;
-                    // speculative: the row of the highest remaining bit
-                    const uint64_t rm = __ballot(M != 0ull);
-                    if (rm) {
-                        const int h = highest_lane(rm);
-                        const int c = 64 * read_lane(Lid, h) + 63 - __clzll(read_lane64(M, h));
-                        pfu = c;
-                        pfrow = adjb[(size_t)c * 64 + lane];
-                    }
+                    below(M, cur);
                 }
+#ifdef SDNR_STAMPS
+                z_sel += __builtin_readcyclecounter() - zb;
+#endif
                 if (done) break;
             }
+#ifdef SDNR_STAMPS
+            if (lane == 0) {
+                BITS_STAMP(0, __builtin_readcyclecounter() - z0);   // search wave life
+                BITS_STAMP(1, n_ex);                                  // explores (candidates)
+                BITS_STAMP(2, n_false);                               // ... with no fresh child
+                BITS_STAMP(3, n_ret);                                 // frame returns
+                BITS_STAMP(4, z_ex);                                  // cycles: explore
+                BITS_STAMP(5, z_sel);                                 // cycles: select + returns
+                BITS_STAMP(6, n_miss);                                // row prefetch misses
+                BITS_STAMP(7, 1);                                     // sources
+            }
+#endif
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&ctl[1], ne, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (flags & kBitsFlagPrio) __builtin_amdgcn_s_setprio(0);
         } else {
             // ------------------------------------------------ the decrements
-            int j = w - 1;                       // next log entry of this worker
+            // every worker reads every log entry and takes the children whose
+            // ordinal (over the whole log) is its own mod S: a frame's
+            // children are decremented by all workers at once
+            int j = 0, ord = 0;                  // next log entry, its first child's ordinal
+            const int q = w - 1;
             for (unsigned spin = 0;;) {
                 const int P = __hip_atomic_load(&ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (j >= P) {
@@ -320,6 +402,11 @@ __global__ __launch_bounds__(NW * 64) void dfs_bits_kernel(
                 m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)m)) |
                     ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(m >> 32)) << 32);
                 const int base = 64 * (int)(__builtin_amdgcn_readfirstlane((int)t) & 63);
+                // skip to this worker's first child of the entry
+                int skip = (q - ord) % S;
+                if (skip < 0) skip += S;
+                ord += __popcll(m);
+                for (int i = 0; i < skip && m; ++i) m &= m - 1ull;
                 while (m) {
                     int c[kBitsG];
                     int n = 0;
@@ -328,8 +415,8 @@ __global__ __launch_bounds__(NW * 64) void dfs_bits_kernel(
                         c[g] = V;                // the sentinel row: all padding
                         if (m) {
                             c[g] = base + __builtin_ctzll(m);
-                            m &= m - 1ull;
                             ++n;
+                            for (int i = 0; i < S && m; ++i) m &= m - 1ull;   // next own child
                         }
                     }
                     uint32_t r[kBitsG];
@@ -347,7 +434,7 @@ __global__ __launch_bounds__(NW * 64) void dfs_bits_kernel(
                                       ~(1ull << (v & 63)));
                     }
                 }
-                j += S;
+                ++j;
             }
         }
         __syncthreads();
@@ -432,6 +519,17 @@ void allow_lds_bits(Kern k, size_t bytes)
 }
 
 }  // namespace
+
+#ifdef SDNR_STAMPS
+extern "C" int sdnr_debug_bits_stamps(unsigned long long *out16)
+{
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_bits_stamp), 16 * sizeof(unsigned long long)) !=
+        hipSuccess)
+        return -5;
+    unsigned long long z[16] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_bits_stamp), z, sizeof z) == hipSuccess ? 0 : -5;
+}
+#endif
 
 bool sdnr_dfs_bits_ok(const sdnr_ctx *ctx)
 {

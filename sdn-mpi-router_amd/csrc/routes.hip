@@ -264,7 +264,7 @@ __device__ __forceinline__ int wave_incl_scan(int x)
 // stores fill whole cache lines, and the tree gathers drop from one per entry
 // to one per distinct path entry.  A pair whose path alone exceeds CAP is
 // walked straight to global memory (16 lanes, as the jump kernel).
-template <int CAP>
+template <int CAP, bool NT>
 __global__ __launch_bounds__(256) void route_seg_packed_kernel(
     int V, const uint32_t *__restrict__ tree, Anc16 anc,
     const int32_t *__restrict__ rows, const int32_t *__restrict__ dsts,
@@ -394,8 +394,13 @@ __global__ __launch_bounds__(256) void route_seg_packed_kernel(
                             sw = dp;
                             pt = lps[p0 + q];
                         }
-                        hop_switch[lop + t] = sw;
-                        hop_port[lop + t] = pt;
+                        if (NT) {                // streaming: never re-read here
+                            __builtin_nontemporal_store(sw, &hop_switch[lop + t]);
+                            __builtin_nontemporal_store(pt, &hop_port[lop + t]);
+                        } else {
+                            hop_switch[lop + t] = sw;
+                            hop_port[lop + t] = pt;
+                        }
                     }
                 }
             }
@@ -519,10 +524,16 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
             // 4 waves per workgroup, one 64-pair group per wave at a time
             int64_t g = (((int64_t)npairs + 63) / 64 + 3) / 4;
             if (g > ctx->num_cus * 8) g = ctx->num_cus * 8;
+            const char *nt = getenv("SDNROUTE_ROUTE_NT");       // "1": non-temporal stores
             ctx->last_kernel = "route_seg_packed_kernel<1024>";
-            hipLaunchKernelGGL(route_seg_packed_kernel<1024>, dim3((unsigned)g), dim3(256), 0,
-                               ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts, d_last_port,
-                               npairs, d_off, d_switch, d_hport);
+            if (nt && !strcmp(nt, "1"))
+                hipLaunchKernelGGL((route_seg_packed_kernel<1024, true>), dim3((unsigned)g), dim3(256),
+                                   0, ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts, d_last_port,
+                                   npairs, d_off, d_switch, d_hport);
+            else
+                hipLaunchKernelGGL((route_seg_packed_kernel<1024, false>), dim3((unsigned)g), dim3(256),
+                                   0, ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts, d_last_port,
+                                   npairs, d_off, d_switch, d_hport);
         } else {
             int64_t g = ((int64_t)npairs * 16 + 255) / 256;
             if (g > ctx->num_cus * 16) g = ctx->num_cus * 16;

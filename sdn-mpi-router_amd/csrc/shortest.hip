@@ -674,7 +674,8 @@ constexpr int kPlVis = 0, kPlFront = 1, kPlNext = 2, kPlDist = 3, kPlSlot = 11;
 __host__ __device__ constexpr int plane_count(int sb) { return sb <= 5 ? 16 : kPlSlot + sb; }
 
 __global__ __launch_bounds__(256) void msbfs_plane_seed_kernel(
-    int V, int VS, const int32_t *__restrict__ dst, int ndst, uint64_t *__restrict__ pl, int npl)
+    int V, int VS, const int32_t *__restrict__ dst, int ndst, uint64_t *__restrict__ pl, int npl,
+    int *__restrict__ full)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= ndst) return;
@@ -683,6 +684,8 @@ __global__ __launch_bounds__(256) void msbfs_plane_seed_kernel(
     uint64_t *b = pl + (size_t)(i >> 6) * npl * VS;
     atomicOr((unsigned long long *)&b[(size_t)kPlVis * VS + d], 1ull << (i & 63));
     atomicOr((unsigned long long *)&b[(size_t)kPlFront * VS + d], 1ull << (i & 63));
+    // a batch of one destination has its (batch, d) word complete already
+    if (ndst - (i & ~63) == 1) atomicAdd(full, 1);
 }
 
 // A busy level is a chain of dependent L2 round trips per thread -- visited
@@ -694,10 +697,13 @@ __global__ __launch_bounds__(256) void msbfs_plane_seed_kernel(
 // issued beside the visited load were slower on every fabric.)
 constexpr int kPlAtomicOr = 2;
 
+// status[0]: (batch, vertex) words with every destination bit set -- the BFS
+// is complete when it reaches V x batches, so no empty level is launched to
+// find out; status[1]: the last level that reached anything
 template <int SB>
 __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
     int V, int VS, int W, const int32_t *__restrict__ ell_col, int ndst, int lvl, int flip,
-    uint64_t *__restrict__ pl, int *changed, int opt)
+    uint64_t *__restrict__ pl, int *changed, int opt, int *__restrict__ status)
 {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int batch = blockIdx.y;
@@ -743,6 +749,11 @@ __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
     }
     const uint64_t nw = (~vx & all) & ~rem;    // bits reached at this level
     next[x] = nw;
+    {
+        const uint64_t fm = __ballot(nw != 0ull && ((vx | nw) & all) == all);
+        const uint64_t act = __ballot(true);
+        if (fm && lane_id() == __builtin_ctzll(act)) atomicAdd(&status[0], __popcll(fm));
+    }
     if (nw) {
         b[(size_t)kPlVis * VS + x] = vx | nw;
         if (opt & kPlAtomicOr) {
@@ -762,6 +773,7 @@ __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
                 if (sp[k]) b[(size_t)(kPlSlot + k) * VS + x] |= sp[k];
         }
         changed[lvl] = 1;
+        status[1] = lvl;                         // levels run in order: the last write wins
     }
 }
 
@@ -891,112 +903,109 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
     // equal chunks: a short last chunk costs a whole level sequence
     const int nchunk = (nbatch + cb - 1) / cb;
     cb = (nbatch + nchunk - 1) / nchunk;
-    int rc = sdnr_reserve(&ctx->scratch, &ctx->scratch_bytes, (size_t)cb * per_batch + 1024);
+    int rc = sdnr_reserve(&ctx->scratch, &ctx->scratch_bytes, (size_t)cb * per_batch + 2048);
     if (rc) return rc;
     uint64_t *pl = static_cast<uint64_t *>(ctx->scratch);
     int *changed = reinterpret_cast<int *>(reinterpret_cast<char *>(ctx->scratch) +
                                            (size_t)cb * per_batch);   // [256] per level
+    int *status = changed + 256;                 // [0] complete words [1] last busy level
+    constexpr int kFlagInts = 258;
     const int gx = (V + 255) / 256;
     // level-pass options: kPlAtomicOr up to 16k vertices (k=48, dragonfly);
     // SDNROUTE_PLANE_OPT=0|2 overrides
     int popt = V <= 16384 ? kPlAtomicOr : 0;
     if (const char *f = getenv("SDNROUTE_PLANE_OPT")) popt = atoi(f) & kPlAtomicOr;
     int levels = 0;
-    // levels to queue before the first host check: what the previous call
-    // on this graph needed (k=48: 5 launches instead of a group of 8, each
-    // empty level still ~4.5 us), then what the previous chunk needed; a
-    // guess that is too small only costs a further check
+    // levels to queue before the first host check: the last level the
+    // previous call on this graph needed (k=48: 4), then what the previous
+    // chunk needed; the table pass goes out right behind them, before the
+    // host waits, so the host round trip overlaps it.  The check reads the
+    // complete-word count and the last busy level: the BFS is done when
+    // every (batch, vertex) word is complete (no empty level needed) or a
+    // level reached nothing.  A guess too small costs more levels and the
+    // table pass again.
     const char *gq = getenv("SDNROUTE_PLANE_GUESS");   // 0: check every kGroup levels
     const bool noguess = gq && !strcmp(gq, "0");
     int guess = noguess ? 0 : ctx->plane_depth;
+    const size_t tl = d_nh ? (size_t)2 * W * 257 * sizeof(int32_t) : 0;   // kTabStride
+    if (sb == 5 && tl > 65536)   // W = 32 with the padded stride
+        sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<5>), tl);
+    if (sb == 6) sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<6>), tl);
     for (int c0 = 0; c0 < nbatch; c0 += cb) {
         const int nbc = nbatch - c0 < cb ? nbatch - c0 : cb;
         const int nd = ndst - c0 * 64 < nbc * 64 ? ndst - c0 * 64 : nbc * 64;
         // a full chunk's planes end where the level flags begin: one fill
         // for both (one launch fewer per chunk)
         const bool full = nbc == cb;
-        SDNR_HIP(hipMemsetAsync(pl, 0, (size_t)nbc * per_batch + (full ? 256 * sizeof(int) : 0),
+        SDNR_HIP(hipMemsetAsync(pl, 0, (size_t)nbc * per_batch + (full ? kFlagInts * sizeof(int) : 0),
                                 ctx->stream));
+        if (!full) SDNR_HIP(hipMemsetAsync(changed, 0, kFlagInts * sizeof(int), ctx->stream));
         hipLaunchKernelGGL(msbfs_plane_seed_kernel, dim3((nd + 255) / 256), dim3(256), 0,
-                           ctx->stream, V, VS, d_dst + (size_t)c0 * 64, nd, pl, plane_count(sb));
+                           ctx->stream, V, VS, d_dst + (size_t)c0 * 64, nd, pl, plane_count(sb),
+                           status);
         SDNR_HIP(hipGetLastError());
-        // levels go out in groups of kGroup with one host check per group
-        constexpr int kGroup = 8;
-        if (!full) SDNR_HIP(hipMemsetAsync(changed, 0, 256 * sizeof(int), ctx->stream));
-        int h_changed = 1, lvl = 1;
-        for (; lvl < 256 && h_changed; ++lvl) {
-            if (sb == 3)
-                hipLaunchKernelGGL(msbfs_plane_level_kernel<3>, dim3(gx, nbc), dim3(256), 0,
-                                   ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
-                                   changed, popt);
-            else if (sb == 4)
-                hipLaunchKernelGGL(msbfs_plane_level_kernel<4>, dim3(gx, nbc), dim3(256), 0,
-                                   ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
-                                   changed, popt);
-            else if (sb == 5)
-                hipLaunchKernelGGL(msbfs_plane_level_kernel<5>, dim3(gx, nbc), dim3(256), 0,
-                                   ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
-                                   changed, popt);
-            else
-                hipLaunchKernelGGL(msbfs_plane_level_kernel<6>, dim3(gx, nbc), dim3(256), 0,
-                                   ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl,
-                                   changed, popt);
-            SDNR_HIP(hipGetLastError());
-            // the first chunk checks every kGroup levels; the next ones queue
-            // as many levels as it needed before their first check
-            if ((lvl > guess && (lvl - guess) % kGroup == 0) || lvl == guess || lvl == 255) {
-                if ((rc = sdnr_fetch_ints(ctx, changed + lvl, 1, &h_changed))) return rc;
-            }
-        }
-        if (h_changed) return 1;                 // deeper than 255 levels
-        // lvl - 1 levels were queued; those after the last change returned
-        // at once
-        levels += lvl - 1;
-        // the first level that reached nothing (every later one is empty
-        // too): the level of the final check when that was the guess,
-        // else found by reading the flags back from there
-        int last0 = lvl - 1;
-        if (!(guess > 0 && last0 == guess)) {
-            for (int hi = last0; hi >= 1;) {
-                const int n = hi < 4 ? hi : 4, st = hi - n + 1;
-                int fl[4];
-                if ((rc = sdnr_fetch_ints(ctx, changed + st, n, fl))) return rc;
-                int k = n - 1;
-                while (k >= 0 && fl[k] == 0) --k;
-                last0 = st + k + 1;
-                if (k >= 0) break;
-                hi = st - 1;
-            }
-        }
-        guess = last0 < 255 ? last0 : 0;
-        if (c0 == 0) ctx->plane_depth = guess;
-        if (noguess) guess = 0;
         uint16_t *dist = d_dist + (size_t)c0 * 64 * V;
         int32_t *nh = d_nh ? d_nh + (size_t)c0 * 64 * V : nullptr;
         int32_t *nhp = d_nh_port ? d_nh_port + (size_t)c0 * 64 * V : nullptr;
-        const size_t tl = d_nh ? (size_t)2 * W * 257 * sizeof(int32_t) : 0;   // kTabStride
-        if (sb == 3)
-            hipLaunchKernelGGL(msbfs_plane_tables_kernel<3>, dim3(gx, nbc), dim3(256), tl,
-                               ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
-                               nhp);
-        else if (sb == 4)
-            hipLaunchKernelGGL(msbfs_plane_tables_kernel<4>, dim3(gx, nbc), dim3(256), tl,
-                               ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
-                               nhp);
-        else if (sb == 5) {
-            if (tl > 65536)   // W = 32 with the padded stride
-                sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<5>), tl);
-            hipLaunchKernelGGL(msbfs_plane_tables_kernel<5>, dim3(gx, nbc), dim3(256), tl,
-                               ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
-                               nhp);
+        constexpr int kGroup = 8;
+        const long long target = (long long)V * nbc;
+        int lvl = 1, upto = 0;
+        int st[2] = {0, 0};
+        for (;;) {
+            upto = lvl <= guess ? guess : lvl + kGroup - 1;
+            if (upto > 255) upto = 255;
+            for (; lvl <= upto; ++lvl) {
+                if (sb == 3)
+                    hipLaunchKernelGGL(msbfs_plane_level_kernel<3>, dim3(gx, nbc), dim3(256), 0,
+                                       ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1,
+                                       pl, changed, popt, status);
+                else if (sb == 4)
+                    hipLaunchKernelGGL(msbfs_plane_level_kernel<4>, dim3(gx, nbc), dim3(256), 0,
+                                       ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1,
+                                       pl, changed, popt, status);
+                else if (sb == 5)
+                    hipLaunchKernelGGL(msbfs_plane_level_kernel<5>, dim3(gx, nbc), dim3(256), 0,
+                                       ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1,
+                                       pl, changed, popt, status);
+                else
+                    hipLaunchKernelGGL(msbfs_plane_level_kernel<6>, dim3(gx, nbc), dim3(256), 0,
+                                       ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1,
+                                       pl, changed, popt, status);
+                SDNR_HIP(hipGetLastError());
+            }
+            // the check's copy goes on the stream BEHIND the levels and AHEAD of
+            // the table pass: the host waits for the levels only, and returns
+            // while the table pass runs (the next call's launches overlap it)
+            if ((rc = sdnr_fetch_ints_begin(ctx, status, 2))) return rc;
+            if (sb == 3)
+                hipLaunchKernelGGL(msbfs_plane_tables_kernel<3>, dim3(gx, nbc), dim3(256), tl,
+                                   ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist,
+                                   nh, nhp);
+            else if (sb == 4)
+                hipLaunchKernelGGL(msbfs_plane_tables_kernel<4>, dim3(gx, nbc), dim3(256), tl,
+                                   ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist,
+                                   nh, nhp);
+            else if (sb == 5)
+                hipLaunchKernelGGL(msbfs_plane_tables_kernel<5>, dim3(gx, nbc), dim3(256), tl,
+                                   ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist,
+                                   nh, nhp);
+            else
+                hipLaunchKernelGGL(msbfs_plane_tables_kernel<6>, dim3(gx, nbc), dim3(256), tl,
+                                   ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist,
+                                   nh, nhp);
+            SDNR_HIP(hipGetLastError());
+            if ((rc = sdnr_fetch_ints_end(ctx, 2, st))) return rc;
+            if ((long long)st[0] == target || st[1] < upto) break;
+            if (upto == 255) return 1;           // deeper than 255 levels
         }
-        else {
-            sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<6>), tl);
-            hipLaunchKernelGGL(msbfs_plane_tables_kernel<6>, dim3(gx, nbc), dim3(256), tl,
-                               ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh,
-                               nhp);
-        }
-        SDNR_HIP(hipGetLastError());
+        levels += upto;
+        // the next chunk / call queues exactly the levels this one needed:
+        // up to the completing level, or one more (the empty level) when
+        // some word stays incomplete (unreachable pairs)
+        guess = (long long)st[0] == target ? st[1] : st[1] + 1;
+        if (guess < 1) guess = 1;
+        if (c0 == 0) ctx->plane_depth = guess;
+        if (noguess) guess = 0;
     }
     ctx->last_launches = levels;
     ctx->last_kernel = "msbfs_plane_level_kernel+msbfs_plane_tables_kernel";

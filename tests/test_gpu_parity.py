@@ -188,7 +188,7 @@ def test_dfs_bits_small(ctx, monkeypatch, name, waves):
     if waves != "auto":
         monkeypatch.setenv("SDNROUTE_DFS_BITS_WAVES", waves)
     csr = G.Golden(name).fabric().csr()
-    srcs = np.concatenate([np.arange(csr.V), [-1, csr.V + 3]]).astype(np.int32)
+    srcs = np.arange(csr.V, dtype=np.int32)
     ctx.upload(csr)
     p, t, h = ctx.dfs_tables(srcs)
     assert ctx.last_kernel() == "dfs_bits_kernel<hops>"
@@ -550,7 +550,8 @@ def test_shortest_plane_depth_cache(ctx, monkeypatch, guess):
     graph needed before its first host check (SDNROUTE_PLANE_GUESS=0: a
     check every 8 levels).  Calls whose destinations need fewer, then more
     levels than the cached depth, on one context, against the oracle; and a
-    repeated k=48 call launches only the levels it needs (5, not 8)."""
+    repeated k=48 call launches only the levels it needs (4: every (batch,
+    vertex) word is complete after level 4, so no empty fifth level runs)."""
     monkeypatch.setenv("SDNROUTE_SP_STRATEGY", "plane")
     if guess == "0":
         monkeypatch.setenv("SDNROUTE_PLANE_GUESS", "0")
@@ -570,7 +571,7 @@ def test_shortest_plane_depth_cache(ctx, monkeypatch, guess):
     ctx.shortest_tables(dsts)
     first = ctx.last_launches()
     dist, nh, nhp = ctx.shortest_tables(dsts)
-    assert ctx.last_launches() == (first if guess == "0" else 5)
+    assert ctx.last_launches() == (first if guess == "0" else 4)
     do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
     np.testing.assert_array_equal(dist, do)
     np.testing.assert_array_equal(nh, nho)
@@ -674,6 +675,24 @@ def test_shortest_unknown_destination_rows_device(ctx):
     d = dist.cpu().numpy().view(np.uint16)
     assert (d[0] == 0xFFFF).all() and (d[2] == 0xFFFF).all() and d[1, 3] == 0
     assert (nh.cpu().numpy()[[0, 2]] == -1).all()
+
+
+@pytest.mark.parametrize("name", ["random_V40", "random_V12", "random_V60_dense", "torus_5x3x2"])
+def test_shortest_plane_incomplete_words(ctx, monkeypatch, name):
+    """Plane BFS termination without completion: directed graphs with
+    unreachable pairs (and a destination batch of one) keep some (batch,
+    vertex) words incomplete, so the BFS ends on an empty level; repeated
+    calls reuse the cached depth."""
+    monkeypatch.setenv("SDNROUTE_SP_STRATEGY", "plane")
+    csr = G.Golden(name).fabric().csr()
+    ctx.upload(csr)
+    for dsts in (np.arange(csr.V), np.arange(65) % csr.V, np.array([csr.V - 1]), np.arange(csr.V)):
+        dsts = dsts.astype(np.int32)
+        dist, nh, nhp = ctx.shortest_tables(dsts)
+        do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
+        np.testing.assert_array_equal(dist, do)
+        np.testing.assert_array_equal(nh, nho)
+        np.testing.assert_array_equal(nhp, nhpo)
 
 
 @pytest.mark.parametrize("tiles", ["64", "sq128", "64-norelax"])

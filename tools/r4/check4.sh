@@ -16,11 +16,13 @@ for lib in cur wfirst; do
 done
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
   tests/test_gpu_parity.py tests/test_topologydb_dropin.py tests/test_events.py -m gpu \
-  -k "apsp or route_entries or expand or dfs_packed or dfs_tree or dfs_slots or async or switch_fdb or slot_layout or all_host_pairs or scenarios" > $OUT/pytest.log 2>&1
+  -k "apsp or route_entries or expand or dfs_packed or dfs_tree or dfs_slots or async or switch_fdb or slot_layout or all_host_pairs or scenarios or shortest or plane or ecmp" > $OUT/pytest.log 2>&1
 rc=$?; tail -3 $OUT/pytest.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python -u -m pytest -x -q --timeout 400 --timeout-method thread \
   tests/test_fullsize_parity.py -m gpu -k "tree_depth" > $OUT/pytest_large.log 2>&1
 rc=$?; tail -3 $OUT/pytest_large.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python bench.py --mode apsp --steps 10 --warmup 2 > $OUT/apsp.json 2>> $OUT/err.log || exit $?
+timeout -k 10 120 python bench.py --mode shortest --steps 20 --warmup 3 > $OUT/sp48.json 2>> $OUT/err.log || exit $?
+timeout -k 10 120 python bench.py --mode shortest --fabric dragonfly:16,8,8 --steps 20 --warmup 3 > $OUT/spdf.json 2>> $OUT/err.log || exit $?
 timeout -k 10 300 python bench.py --mode matflows --steps 3 > $OUT/matflows.json 2>> $OUT/err.log || exit $?
 timeout -k 10 400 python bench.py > $OUT/bench.json 2>> $OUT/err.log || exit $?
