@@ -228,6 +228,16 @@ int sdnr_route_expand(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port,
                       const int64_t *offsets, int32_t *hop_switch,
                       int32_t *hop_port, uint32_t flags);
 
+/* The same entries as ONE u32 word each, switch | out_port << 16 (the
+ * packed tree word's layout: a dense switch id and a 16-bit OpenFlow 1.0
+ * port, OFPP_LOCAL = 0xfffe included) -- half the bytes of the two int32
+ * arrays.  Needs V <= 65535, 16-bit ports and last ports <= 0xffff; device
+ * pointers only (flags must hold SDNR_DEVICE_PTRS). */
+int sdnr_route_expand_packed(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port,
+                             int32_t nrows, const int32_t *rows, const int32_t *dsts,
+                             const int32_t *last_port, int32_t npairs, const int64_t *offsets,
+                             uint32_t *entries, uint32_t flags);
+
 /* Flood ports (TopologyManager._is_edge_port / _do_broadcast, reference
  * sdnmpi/topology.py:150-177): is_edge[i] = 1 iff ports[i] is neither end of
  * any link.  Keys are (dense switch id << 32) | port_no; ends (both ends of

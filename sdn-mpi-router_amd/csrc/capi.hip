@@ -1008,6 +1008,22 @@ int sdnr_route_offsets(sdnr_ctx *ctx, const int32_t *hops, int32_t nrows, const 
     return SDNR_OK;
 }
 
+int sdnr_route_expand_packed(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port,
+                             int32_t nrows, const int32_t *rows, const int32_t *dsts,
+                             const int32_t *last_port, int32_t npairs, const int64_t *offsets,
+                             uint32_t *entries, uint32_t flags)
+{
+    int rc = begin_call(ctx, 0, nullptr, flags, "sdnr_route_expand_packed");
+    if (rc) return rc;
+    if (!(flags & SDNR_DEVICE_PTRS))
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_route_expand_packed: device pointers only");
+    if (npairs < 0 || nrows < 0 || !offsets ||
+        (npairs > 0 && (!parent || !port || !rows || !dsts || !last_port || !entries)))
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_route_expand_packed: bad arguments");
+    return sdnr_launch_route_expand(ctx, parent, port, nrows, rows, dsts, last_port, npairs,
+                                    offsets, nullptr, nullptr, entries);
+}
+
 int sdnr_route_expand(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port, int32_t nrows,
                       const int32_t *rows, const int32_t *dsts, const int32_t *last_port,
                       int32_t npairs, const int64_t *offsets, int32_t *hop_switch,

@@ -169,6 +169,6 @@ int sdnr_launch_route_offsets(sdnr_ctx *ctx, const int32_t *d_hops, const int32_
 int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32_t *d_port,
                              int32_t nrows, const int32_t *d_rows, const int32_t *d_dsts,
                              const int32_t *d_last_port, int32_t npairs, const int64_t *d_off,
-                             int32_t *d_switch, int32_t *d_hport);
+                             int32_t *d_switch, int32_t *d_hport, uint32_t *d_entries = nullptr);
 int sdnr_launch_edge_ports(sdnr_ctx *ctx, const uint64_t *d_ends, int32_t nends,
                            const uint64_t *d_ports, int32_t nports, uint8_t *d_is_edge);

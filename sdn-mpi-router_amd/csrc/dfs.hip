@@ -1649,41 +1649,17 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
             SDNR_STAMP(st_t0);
             st_tc = st_t0;
 #endif
-            int nu = -1;        // next candidate found among the newest children
-            for (;;) {
-                int u;
-                if (nu >= 0) {
-                    u = nu;
-                    nu = -1;
-                } else {
-                    uint64_t m = 0;
-                    int e = V;
-                    while (sp > 0) {
-#ifdef SDNR_STAMPS
-                        st_skip++;
+            // one candidate: its row, fresh children, push; returns the
+            // next candidate when it is one of the new children (the
+            // common case: a tight inner loop), else -1 (pop from the stack)
+#ifdef SDNR_ASYNC_SPEC
+            // speculative visited gather of the top child (su: its vertex, sx
+            // its row, swv the gathered visited words), issued right behind
+            // the push's marks; used when that child is the next candidate
+            int su = -1, sx = 0;
+            uint32_t swv = 0u;
 #endif
-                        const int kk = sp < 64 ? sp : 64;
-                        const int at = sp - 1 - lane;
-                        e = stk[at < 0 ? 0 : at];
-                        e = lane < kk ? e : V;
-                        const uint32_t c = cnt_of(e);
-                        m = __ballot(c != 0u);
-                        if (m) break;
-                        sp -= kk;
-                    }
-                    // children of the last push not yet announced (the push
-                    // block announces its own; kept for the first pops)
-                    if (pub != pubd) {
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-                        if (lane == 0) __hip_atomic_store(&ctl[0], pub, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_WORKGROUP);
-                        pubd = pub;
-                    }
-                    if (!m) break;
-                    const int first = __ffsll((unsigned long long)m) - 1;
-                    u = read_lane(e, first);
-                    sp -= first + 1;
-                }
+            auto explore = [&](const int u) -> int {
 #ifdef SDNR_STAMPS
                 unsigned long long ta, tb;
                 SDNR_STAMP(ta);
@@ -1696,11 +1672,22 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                 }
 #endif
                 int x = -1;
+                uint32_t wv;
+#ifdef SDNR_ASYNC_SPEC
+                const bool spec = u == su;
+                su = -1;
+                if (spec) {
+                    x = sx;
+                    wv = swv;
+                } else
+#endif
+                {
 #pragma unroll
-                for (int k = 0; k < NPF; ++k)
-                    if (x < 0 && u == pu[k]) x = (int)xp[k];
-                if (x < 0) x = (int)adj[(size_t)u * 64 + lane];
-                const uint32_t wv = vis[x >> 5];
+                    for (int k = 0; k < NPF; ++k)
+                        if (x < 0 && u == pu[k]) x = (int)xp[k];
+                    if (x < 0) x = (int)adj[(size_t)u * 64 + lane];
+                    wv = vis[x >> 5];
+                }
                 const bool fresh = ((wv >> (x & 31)) & 1u) == 0u;
                 const uint64_t mm = __ballot(fresh);
 #ifdef SDNR_STAMPS
@@ -1712,7 +1699,7 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
 #ifdef SDNR_STAMPS
                 if (mm == 0) st_tc = tb;
 #endif
-                if (mm == 0) continue;           // stale count: a leaf pop after all
+                if (mm == 0) return -1;          // stale count: a leaf pop after all
                 const int c = __popcll(mm);
                 const int rank = lanes_below(mm);
                 // the next candidates are most likely the newest children
@@ -1740,6 +1727,7 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                     for (int q = 0; q < S; ++q)
                         lo = min(lo, __hip_atomic_load(&ctl[2 + q], __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_WORKGROUP));
+                    lo = uniform(lo);            // scalar: the bound test stays off the VALU
                     if (pub + c - lo <= RING) break;
                     if (spin > kSpin) {
                         if (lane == 0) atomicOr(err, 1);
@@ -1754,9 +1742,11 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                 // the children's counts are read FIRST: LDS ops complete in
                 // order, so behind the mark / stack / ring / parent writes the
                 // gather waited for all four; issued before them it returns
-                // while they drain (the next row wait hides them)
+                // while they drain.  Read in every lane (x <= V is always a
+                // count word): under `if (fresh)` the compiler closed the
+                // masked block with the wait, before the writes were issued
 #ifndef SDNR_AB_WRITES_FIRST
-                if (fresh) cc = cnt_of(x);
+                cc = cnt_of(x);
 #endif
                 if (fresh) {
                     atomicOr(&vis[x >> 5], 1u << (x & 31));
@@ -1782,8 +1772,16 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                 __asm__ volatile("" ::: "memory");
                 if (lane == 0) __hip_atomic_store(&ctl[0], pub, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-                const uint64_t mc = __ballot(cc != 0u);
+#ifdef SDNR_ASYNC_SPEC
+                if (pu[0] >= 0) {
+                    su = pu[0];
+                    sx = (int)xp[0];
+                    swv = vis[sx >> 5];
+                }
+#endif
+                const uint64_t mc = __ballot(cc != 0u) & mm;     // fresh children with a count
                 pubd = pub;
+                int nu = -1;
                 if (mc) {
                     // children above the highest one with a count are leaves
                     // (counts are never low): popped; it is the next candidate
@@ -1795,6 +1793,36 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                 SDNR_STAMP(st_tc);
                 st_pushc += st_tc - tb;
 #endif
+                return nu;
+            };
+            for (;;) {
+                uint64_t m = 0;
+                int e = V;
+                while (sp > 0) {
+#ifdef SDNR_STAMPS
+                    st_skip++;
+#endif
+                    const int kk = sp < 64 ? sp : 64;
+                    const int at = sp - 1 - lane;
+                    e = stk[at < 0 ? 0 : at];
+                    e = lane < kk ? e : V;
+                    const uint32_t c = cnt_of(e);
+                    m = __ballot(c != 0u);
+                    if (m) break;
+                    sp -= kk;
+                }
+                // children of the last push not yet announced (the push
+                // block announces its own; kept for the first pops)
+                if (pub != pubd) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                    if (lane == 0) __hip_atomic_store(&ctl[0], pub, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                    pubd = pub;
+                }
+                if (!m) break;
+                const int first = __ffsll((unsigned long long)m) - 1;
+                sp -= first + 1;
+                for (int u = read_lane(e, first); u >= 0;) u = explore(u);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_store(&ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

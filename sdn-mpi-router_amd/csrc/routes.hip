@@ -264,7 +264,9 @@ __device__ __forceinline__ int wave_incl_scan(int x)
 // stores fill whole cache lines, and the tree gathers drop from one per entry
 // to one per distinct path entry.  A pair whose path alone exceeds CAP is
 // walked straight to global memory (16 lanes, as the jump kernel).
-template <int CAP, bool NT>
+// OUTP: entries as one u32 each, switch | port << 16 (the tree word layout:
+// the LDS buffer is copied as is) instead of two int32 arrays
+template <int CAP, bool NT, bool OUTP>
 __global__ __launch_bounds__(256) void route_seg_packed_kernel(
     int V, const uint32_t *__restrict__ tree, Anc16 anc,
     const int32_t *__restrict__ rows, const int32_t *__restrict__ dsts,
@@ -313,9 +315,14 @@ __global__ __launch_bounds__(256) void route_seg_packed_kernel(
                 if (lane < 16) {
                     const int k = lane;
                     int y = read_lane(d, 0);
+                    uint32_t *ent = reinterpret_cast<uint32_t *>(hop_switch);
                     if (k == 0) {
-                        hop_switch[lo0 + h] = y;
-                        hop_port[lo0 + h] = read_lane(lp, 0);
+                        if (OUTP) {
+                            ent[lo0 + h] = (uint32_t)y | ((uint32_t)read_lane(lp, 0) << 16);
+                        } else {
+                            hop_switch[lo0 + h] = y;
+                            hop_port[lo0 + h] = read_lane(lp, 0);
+                        }
                     }
                     if (k < h) {
                         if (k & 1) y = (int)(tree[rb + y] & 0xFFFFu);
@@ -324,8 +331,12 @@ __global__ __launch_bounds__(256) void route_seg_packed_kernel(
                             if (k & (1 << j)) y = anc.a[j][rb + y];
                         for (int u = k; u < h; u += 16) {
                             const uint32_t e = tree[rb + y];
-                            hop_switch[lo0 + h - u - 1] = (int32_t)(e & 0xFFFFu);
-                            hop_port[lo0 + h - u - 1] = (int32_t)(e >> 16);
+                            if (OUTP) {
+                                ent[lo0 + h - u - 1] = e;
+                            } else {
+                                hop_switch[lo0 + h - u - 1] = (int32_t)(e & 0xFFFFu);
+                                hop_port[lo0 + h - u - 1] = (int32_t)(e >> 16);
+                            }
                             if (u + 16 < h) y = anc16[rb + y];
                         }
                     }
@@ -386,6 +397,12 @@ __global__ __launch_bounds__(256) void route_seg_packed_kernel(
                         if (k >= Lr) { ++q; k -= Lr; }
                         if (k < 0) { --q; k += Lr; }
                         int sw, pt;
+                        if (OUTP) {
+                            const uint32_t e = k < Lr - 1 ? buf[sop + k]
+                                                          : (uint32_t)dp | ((uint32_t)lps[p0 + q] << 16);
+                            reinterpret_cast<uint32_t *>(hop_switch)[lop + t] = e;
+                            continue;
+                        }
                         if (k < Lr - 1) {
                             const uint32_t e = buf[sop + k];
                             sw = (int)(e & 0xFFFFu);
@@ -488,9 +505,11 @@ int sdnr_launch_route_offsets(sdnr_ctx *ctx, const int32_t *d_hops, const int32_
 int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32_t *d_port,
                              int32_t nrows, const int32_t *d_rows, const int32_t *d_dsts,
                              const int32_t *d_last_port, int32_t npairs, const int64_t *d_off,
-                             int32_t *d_switch, int32_t *d_hport)
+                             int32_t *d_switch, int32_t *d_hport, uint32_t *d_entries)
 {
     if (npairs == 0) return SDNR_OK;
+    if (d_entries && !(ctx->V <= 0xFFFF && ctx->port16))
+        return sdnr_fail(SDNR_ERR_INVAL, "route entries as u32 need V <= 65535 and 16-bit ports");
     const char *f = getenv("SDNROUTE_ROUTE_WALK");      // "serial": one lane per pair
     const bool serial = f && !strcmp(f, "serial");
     const size_t n = (size_t)nrows * (size_t)ctx->V;
@@ -503,7 +522,8 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
     }
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
     const char *pk = getenv("SDNROUTE_ROUTE_PACKED");          // "0": int32 tables
-    const bool packed = !serial && ctx->V <= 0xFFFF && ctx->port16 && !(pk && !strcmp(pk, "0"));
+    const bool packed = d_entries ||
+                        (!serial && ctx->V <= 0xFFFF && ctx->port16 && !(pk && !strcmp(pk, "0")));
     if (packed) {
         // scratch2 (14n bytes): tree u32 [n] | u16 ancestor tables a1..a16 [n]
         uint32_t *tree = reinterpret_cast<uint32_t *>(anc);
@@ -520,20 +540,28 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
             tabs.a[j] = o;
         }
         const char *sg = getenv("SDNROUTE_ROUTE_SEG");        // "0": per-entry jump walks
-        if (!(sg && !strcmp(sg, "0"))) {
+        if (d_entries || !(sg && !strcmp(sg, "0"))) {
             // 4 waves per workgroup, one 64-pair group per wave at a time
             int64_t g = (((int64_t)npairs + 63) / 64 + 3) / 4;
             if (g > ctx->num_cus * 8) g = ctx->num_cus * 8;
             const char *nt = getenv("SDNROUTE_ROUTE_NT");       // "1": non-temporal stores
-            ctx->last_kernel = "route_seg_packed_kernel<1024>";
-            if (nt && !strcmp(nt, "1"))
-                hipLaunchKernelGGL((route_seg_packed_kernel<1024, true>), dim3((unsigned)g), dim3(256),
-                                   0, ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts, d_last_port,
-                                   npairs, d_off, d_switch, d_hport);
-            else
-                hipLaunchKernelGGL((route_seg_packed_kernel<1024, false>), dim3((unsigned)g), dim3(256),
-                                   0, ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts, d_last_port,
-                                   npairs, d_off, d_switch, d_hport);
+            if (d_entries) {
+                ctx->last_kernel = "route_seg_packed_kernel<1024,u32>";
+                hipLaunchKernelGGL((route_seg_packed_kernel<1024, false, true>), dim3((unsigned)g),
+                                   dim3(256), 0, ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts,
+                                   d_last_port, npairs, d_off, reinterpret_cast<int32_t *>(d_entries),
+                                   nullptr);
+            } else {
+                ctx->last_kernel = "route_seg_packed_kernel<1024>";
+                if (nt && !strcmp(nt, "1"))
+                    hipLaunchKernelGGL((route_seg_packed_kernel<1024, true, false>), dim3((unsigned)g),
+                                       dim3(256), 0, ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts,
+                                       d_last_port, npairs, d_off, d_switch, d_hport);
+                else
+                    hipLaunchKernelGGL((route_seg_packed_kernel<1024, false, false>), dim3((unsigned)g),
+                                       dim3(256), 0, ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts,
+                                       d_last_port, npairs, d_off, d_switch, d_hport);
+            }
         } else {
             int64_t g = ((int64_t)npairs * 16 + 255) / 256;
             if (g > ctx->num_cus * 16) g = ctx->num_cus * 16;

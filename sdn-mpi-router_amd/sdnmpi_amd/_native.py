@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = (
     "sdnr_abi_version", "sdnr_last_error", "sdnr_device_count", "sdnr_create",
     "sdnr_create_multi", "sdnr_device_list", "sdnr_destroy", "sdnr_set_stream", "sdnr_synchronize", "sdnr_graph_upload",
     "sdnr_graph_info", "sdnr_dfs_tables", "sdnr_dfs_tables_packed", "sdnr_dfs_tables_slots",
-    "sdnr_dfs_tables_tree", "sdnr_tree_pack", "sdnr_shortest_tables",
+    "sdnr_dfs_tables_tree", "sdnr_tree_pack", "sdnr_shortest_tables", "sdnr_route_expand_packed",
     "sdnr_apsp", "sdnr_route_offsets", "sdnr_route_expand", "sdnr_ecmp_counts",
     "sdnr_ecmp_routes",
     "sdnr_last_kernel_ms", "sdnr_last_kernel", "sdnr_last_launches", "sdnr_last_sweeps",
@@ -82,6 +82,7 @@ def _bind(L):
         "sdnr_dfs_tables_slots": ([vp, vp, i32, vp, u32], c_int),
         "sdnr_tree_pack": ([vp, vp, vp, ctypes.c_int64, vp, i32, u32], c_int),
         "sdnr_dfs_tables_tree": ([vp, vp, i32, vp, vp, i32, i32, u32], c_int),
+        "sdnr_route_expand_packed": ([vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, u32], c_int),
         "sdnr_shortest_tables": ([vp, vp, i32, vp, vp, vp, u32], c_int),
         "sdnr_apsp": ([vp, vp, u32], c_int),
         "sdnr_route_offsets": ([vp, vp, i32, vp, vp, i32, vp, u32], c_int),
@@ -350,6 +351,16 @@ class Context(object):
                                            ctypes.c_void_p(dsts_ptr), ctypes.c_void_p(last_ptr),
                                            int(npairs), ctypes.c_void_p(off_ptr),
                                            ctypes.c_void_p(sw_ptr), ctypes.c_void_p(hp_ptr), flags))
+
+    def expand_routes_packed_device(self, parent_ptr, port_ptr, nrows, rows_ptr, dsts_ptr,
+                                    last_ptr, npairs, off_ptr, ent_ptr, timing=False):
+        """Flow entries as one u32 each, switch | port << 16
+        (sdnr_route_expand_packed, device pointers)."""
+        flags = DEVICE_PTRS | (TIMING if timing else 0)
+        _check(self._lib.sdnr_route_expand_packed(
+            self._h, ctypes.c_void_p(parent_ptr), ctypes.c_void_p(port_ptr), int(nrows),
+            ctypes.c_void_p(rows_ptr), ctypes.c_void_p(dsts_ptr), ctypes.c_void_p(last_ptr),
+            int(npairs), ctypes.c_void_p(off_ptr), ctypes.c_void_p(ent_ptr), flags))
 
     def edge_ports(self, ends, ports):
         """bool [n_ports]: ports (uint64 keys) that are no link end (``ends``:

@@ -440,6 +440,23 @@ class RouteEngine(object):
         self.ctx.synchronize()
         off = d_off.cpu().numpy()
         total = int(off[-1])
+        lp = np.asarray(last_port)
+        env = os.environ.get
+        if tree_layout(export.csr) == PORT16 and (lp.size == 0 or
+                                                  (lp.min() >= 0 and lp.max() <= 0xFFFF)) \
+                and env("SDNROUTE_ROUTE_OUT", "") != "int32" \
+                and env("SDNROUTE_ROUTE_WALK", "") != "serial" and env("SDNROUTE_ROUTE_SEG", "") != "0" \
+                and env("SDNROUTE_ROUTE_PACKED", "") != "0":
+            # one u32 per entry (switch | port << 16): half the bytes written
+            # and copied back; split on the host
+            ent = t.empty(max(total, 1), dtype=t.int32, device=self.dev)
+            self.ctx.expand_routes_packed_device(par.data_ptr(), prt.data_ptr(), nrows,
+                                                 d_rows.data_ptr(), d_dsts.data_ptr(),
+                                                 d_last.data_ptr(), n, d_off.data_ptr(),
+                                                 ent.data_ptr())
+            self.ctx.synchronize()
+            e = ent[:total].cpu().numpy().view(np.uint32)
+            return off, (e & 0xFFFF).astype(np.int32), (e >> 16).astype(np.int32)
         sw = t.empty(max(total, 1), dtype=t.int32, device=self.dev)
         hp = t.empty(max(total, 1), dtype=t.int32, device=self.dev)
         self.ctx.expand_routes_device(par.data_ptr(), prt.data_ptr(), nrows,

@@ -320,7 +320,7 @@ def test_route_entries_batched_fake_engine():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("walk", ["auto", "jump16", "serial", "int32", "p4", "p8"])
+@pytest.mark.parametrize("walk", ["auto", "seg32", "jump16", "serial", "int32", "p4", "p8"])
 @pytest.mark.parametrize("name", ["mock", "fat_tree_k8", "dragonfly_a4_h2_p2", "random_V40",
                                   "torus_5x3x2"])
 def test_route_entries_match_reference(monkeypatch, name, walk):
@@ -331,6 +331,8 @@ def test_route_entries_match_reference(monkeypatch, name, walk):
         monkeypatch.setenv("SDNROUTE_ROUTE_WALK", walk)
     elif walk == "jump16":                       # packed per-entry jump walks
         monkeypatch.setenv("SDNROUTE_ROUTE_SEG", "0")
+    elif walk == "seg32":                        # entries as two int32 arrays
+        monkeypatch.setenv("SDNROUTE_ROUTE_OUT", "int32")
     elif walk != "auto":                         # int32-table jump kernels
         monkeypatch.setenv("SDNROUTE_ROUTE_PACKED", "0")
         if walk != "int32":
@@ -364,10 +366,16 @@ def test_route_entries_k48_many_pairs(monkeypatch):
     assert db.engine.ctx.last_kernel() == "route_walk_kernel"
     monkeypatch.delenv("SDNROUTE_ROUTE_WALK")
     o1, d1, p1 = db.route_entries(pairs)
-    assert db.engine.ctx.last_kernel() == "route_seg_packed_kernel<1024>"
+    assert db.engine.ctx.last_kernel() == "route_seg_packed_kernel<1024,u32>"
     np.testing.assert_array_equal(o0, o1)
     np.testing.assert_array_equal(d0, d1)
     np.testing.assert_array_equal(p0, p1)
+    monkeypatch.setenv("SDNROUTE_ROUTE_OUT", "int32")
+    o3, d3, p3 = db.route_entries(pairs)
+    assert db.engine.ctx.last_kernel() == "route_seg_packed_kernel<1024>"
+    np.testing.assert_array_equal(o0, o3)
+    np.testing.assert_array_equal(d0, d3)
+    np.testing.assert_array_equal(p0, p3)
     monkeypatch.setenv("SDNROUTE_ROUTE_SEG", "0")
     o2, d2, p2 = db.route_entries(pairs)
     assert db.engine.ctx.last_kernel() == "route_jump_packed_kernel<16>"
@@ -401,7 +409,12 @@ def test_route_entries_runs_and_long_paths(monkeypatch, fab):
     o0, d0, p0 = db.route_entries(pairs)
     monkeypatch.delenv("SDNROUTE_ROUTE_WALK")
     o1, d1, p1 = db.route_entries(pairs)
+    assert db.engine.ctx.last_kernel() == "route_seg_packed_kernel<1024,u32>"
+    monkeypatch.setenv("SDNROUTE_ROUTE_OUT", "int32")
+    o2, d2, p2 = db.route_entries(pairs)
     assert db.engine.ctx.last_kernel() == "route_seg_packed_kernel<1024>"
+    for a, b in ((o1, o2), (d1, d2), (p1, p2)):
+        np.testing.assert_array_equal(a, b)
     if not fab.startswith("fat"):
         assert int(np.diff(o0).max()) > 1024     # some pairs take the direct walk
     np.testing.assert_array_equal(o0, o1)

@@ -1,6 +1,7 @@
 #!/bin/bash
 # round 4: bits kernel v2 (batch candidate tests, per-child worker split): parity, anatomy, A/B
 OUT=gpurun_out/r4_c6; mkdir -p $OUT
+timeout -k 10 60 tools/r4/chain_probe > $OUT/chain.log 2>&1 || exit $?
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
   tests/test_gpu_parity.py -m gpu -k "dfs_bits" > $OUT/pytest_bits.log 2>&1
 rc=$?; tail -3 $OUT/pytest_bits.log; [ $rc -eq 0 ] || exit $rc

@@ -16,6 +16,10 @@ for f in sorted(glob.glob(os.path.join(d, "*.json"))):
     if "materialised_flows" in j:
         m = j["materialised_flows"]
         extra += " matflows %.1f ms" % m["ms"]
+    if "materialised_flows_packed" in j:
+        extra += " packed %.1f ms" % j["materialised_flows_packed"]["ms"]
+    if "packed_all_ms" in j:
+        extra += " packed_all_ms %s" % ["%.1f" % x for x in j["packed_all_ms"]]
     if "all_ms" in j:
         extra += " all_ms %s" % ["%.1f" % x for x in j["all_ms"]]
     print("%-24s ms/step %8.4f kern %8.4f frac %.3f %s%s" % (
