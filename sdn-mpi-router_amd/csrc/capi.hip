@@ -66,17 +66,29 @@ int sdnr_reserve(void **buf, size_t *cur, size_t need)
     return SDNR_OK;
 }
 
-int sdnr_fetch_ints_begin(sdnr_ctx *ctx, const int *d_src, int n)
+int sdnr_wait_published(sdnr_ctx *ctx, int seq, int n, int *out)
+{
+    volatile int *h = ctx->h_pub;
+    for (unsigned k = 0;; ++k) {
+        if (__atomic_load_n(&h[3], __ATOMIC_ACQUIRE) == seq) break;
+        if ((k & 63) == 63) {                    // the stream drained without publishing: fault
+            const hipError_t e = hipStreamQuery(ctx->stream);
+            if (e == hipSuccess && __atomic_load_n(&h[3], __ATOMIC_ACQUIRE) != seq)
+                return sdnr_fail(SDNR_ERR_HIP, "sdnr_wait_published: stream idle, word %d not "
+                                                "published", seq);
+            if (e != hipSuccess && e != hipErrorNotReady) return sdnr_hip_fail(e, "sdnr_wait_published");
+        }
+    }
+    for (int i = 0; i < n; ++i) out[i] = h[i];
+    return SDNR_OK;
+}
+
+int sdnr_fetch_ints(sdnr_ctx *ctx, const int *d_src, int n, int *out)
 {
     if (n < 1 || n > 4) return sdnr_fail(SDNR_ERR_INVAL, "sdnr_fetch_ints: %d words", n);
     SDNR_HIP(hipMemcpyAsync(ctx->h_flag, d_src, (size_t)n * sizeof(int), hipMemcpyDeviceToHost,
                             ctx->stream));
     SDNR_HIP(hipEventRecord(ctx->ev_flag, ctx->stream));
-    return SDNR_OK;
-}
-
-int sdnr_fetch_ints_end(sdnr_ctx *ctx, int n, int *out)
-{
     for (;;) {
         const hipError_t e = hipEventQuery(ctx->ev_flag);
         if (e == hipSuccess) break;
@@ -84,12 +96,6 @@ int sdnr_fetch_ints_end(sdnr_ctx *ctx, int n, int *out)
     }
     for (int i = 0; i < n; ++i) out[i] = reinterpret_cast<volatile int *>(ctx->h_flag)[i];
     return SDNR_OK;
-}
-
-int sdnr_fetch_ints(sdnr_ctx *ctx, const int *d_src, int n, int *out)
-{
-    const int rc = sdnr_fetch_ints_begin(ctx, d_src, n);
-    return rc ? rc : sdnr_fetch_ints_end(ctx, n, out);
 }
 
 static void free_graph(sdnr_ctx *c)
@@ -220,6 +226,12 @@ int sdnr_create(int device, sdnr_ctx **out)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_flag, hipEventDisableTiming);
     if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&c->h_flag), 4 * sizeof(int));
+    // fine-grained (coherent) host words: a kernel's system-scope stores reach
+    // the host without a copy on the stream
+    if (e == hipSuccess)
+        e = hipHostMalloc(reinterpret_cast<void **>(&c->h_pub), 64,
+                          hipHostMallocCoherent | hipHostMallocMapped);
+    if (e == hipSuccess) memset(c->h_pub, 0, 64);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&c->d_err), sizeof(int));
     if (e == hipSuccess) e = hipMemset(c->d_err, 0, sizeof(int));
     if (e != hipSuccess) {
@@ -288,6 +300,7 @@ int sdnr_destroy(sdnr_ctx *ctx)
     if (ctx->stage) (void)hipFree(ctx->stage);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->h_flag) (void)hipHostFree(ctx->h_flag);
+    if (ctx->h_pub) (void)hipHostFree(ctx->h_pub);
     if (ctx->ev_flag) (void)hipEventDestroy(ctx->ev_flag);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);

@@ -96,6 +96,8 @@ struct sdnr_ctx {
     int32_t plane_depth = 0;            // levels the bit-plane BFS last needed on this graph
     int *d_err = nullptr;               // kernel watchdog word (0 = ok)
     int *h_flag = nullptr;              // pinned host words for level-loop checks
+    int *h_pub = nullptr;               // coherent host words a kernel publishes into
+    int pub_seq = 0;                    // sequence number of the last publication
     hipEvent_t ev_flag = nullptr;       // ... and the event the host spins on
 
     // multi-device context (sdnr_create_multi): this context is shard 0 on
@@ -128,8 +130,7 @@ int sdnr_check_watchdog(sdnr_ctx *ctx);   // after a stream sync
 int sdnr_fetch_ints(sdnr_ctx *ctx, const int *d_src, int n, int *out);
 // the same in two halves: the copy + event go on the stream, more work may
 // follow them, then the host waits for the event (the words as of then)
-int sdnr_fetch_ints_begin(sdnr_ctx *ctx, const int *d_src, int n);
-int sdnr_fetch_ints_end(sdnr_ctx *ctx, int n, int *out);
+int sdnr_wait_published(sdnr_ctx *ctx, int seq, int n, int *out);
 
 #define SDNR_HIP(call)                                           \
     do {                                                         \

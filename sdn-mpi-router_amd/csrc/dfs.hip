@@ -1652,13 +1652,6 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
             // one candidate: its row, fresh children, push; returns the
             // next candidate when it is one of the new children (the
             // common case: a tight inner loop), else -1 (pop from the stack)
-#ifdef SDNR_ASYNC_SPEC
-            // speculative visited gather of the top child (su: its vertex, sx
-            // its row, swv the gathered visited words), issued right behind
-            // the push's marks; used when that child is the next candidate
-            int su = -1, sx = 0;
-            uint32_t swv = 0u;
-#endif
             auto explore = [&](const int u) -> int {
 #ifdef SDNR_STAMPS
                 unsigned long long ta, tb;
@@ -1672,22 +1665,11 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                 }
 #endif
                 int x = -1;
-                uint32_t wv;
-#ifdef SDNR_ASYNC_SPEC
-                const bool spec = u == su;
-                su = -1;
-                if (spec) {
-                    x = sx;
-                    wv = swv;
-                } else
-#endif
-                {
 #pragma unroll
-                    for (int k = 0; k < NPF; ++k)
-                        if (x < 0 && u == pu[k]) x = (int)xp[k];
-                    if (x < 0) x = (int)adj[(size_t)u * 64 + lane];
-                    wv = vis[x >> 5];
-                }
+                for (int k = 0; k < NPF; ++k)
+                    if (x < 0 && u == pu[k]) x = (int)xp[k];
+                if (x < 0) x = (int)adj[(size_t)u * 64 + lane];
+                const uint32_t wv = vis[x >> 5];
                 const bool fresh = ((wv >> (x & 31)) & 1u) == 0u;
                 const uint64_t mm = __ballot(fresh);
 #ifdef SDNR_STAMPS
@@ -1738,16 +1720,13 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
 #endif
                     __builtin_amdgcn_s_sleep(1);
                 }
-                uint32_t cc = 0u;
                 // the children's counts are read FIRST: LDS ops complete in
                 // order, so behind the mark / stack / ring / parent writes the
                 // gather waited for all four; issued before them it returns
                 // while they drain.  Read in every lane (x <= V is always a
                 // count word): under `if (fresh)` the compiler closed the
                 // masked block with the wait, before the writes were issued
-#ifndef SDNR_AB_WRITES_FIRST
-                cc = cnt_of(x);
-#endif
+                const uint32_t cc = cnt_of(x);
                 if (fresh) {
                     atomicOr(&vis[x >> 5], 1u << (x & 31));
                     if (C16) {
@@ -1759,9 +1738,6 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                     if (HOPS) dep[x] = (uint16_t)(du + 1);
                     stk[sp + rank] = (uint16_t)x;
                     ring[(pub + rank) & (RING - 1)] = (uint16_t)x;
-#ifdef SDNR_AB_WRITES_FIRST   // A/B build: the round-3 push (count after the writes)
-                    cc = cnt_of(x);
-#endif
                 }
                 pub += c;
                 // announce the children without waiting for the writes: one
@@ -1772,13 +1748,6 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                 __asm__ volatile("" ::: "memory");
                 if (lane == 0) __hip_atomic_store(&ctl[0], pub, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-#ifdef SDNR_ASYNC_SPEC
-                if (pu[0] >= 0) {
-                    su = pu[0];
-                    sx = (int)xp[0];
-                    swv = vis[sx >> 5];
-                }
-#endif
                 const uint64_t mc = __ballot(cc != 0u) & mm;     // fresh children with a count
                 pubd = pub;
                 int nu = -1;

@@ -688,6 +688,46 @@ __global__ __launch_bounds__(256) void msbfs_plane_seed_kernel(
     if (ndst - (i & ~63) == 1) atomicAdd(full, 1);
 }
 
+// the planes of a chunk zeroed, the destinations seeded into the visited and
+// frontier planes, the level flags and status words reset -- one launch in
+// place of two fills and the seed kernel.  Thread (batch, x) writes column x
+// (pad words included) of every plane of its batch.
+__global__ __launch_bounds__(256) void msbfs_plane_init_kernel(
+    int V, int VS, const int32_t *__restrict__ dst, int ndst, uint64_t *__restrict__ pl, int npl,
+    int *__restrict__ flags, int nflags, int *__restrict__ status)
+{
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int batch = blockIdx.y;
+    const int nb = min(64, ndst - batch * 64);
+    const int lane = lane_id();
+    const int mine = lane < nb ? dst[batch * 64 + lane] : -1;
+    // the batch's id range (wave reductions): a wave outside it skips the
+    // 64-step match (destination lists are usually runs of ids)
+    int lo = mine >= 0 ? mine : 0x7FFFFFFF, hi = mine;
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, __shfl_xor(lo, o));
+        hi = max(hi, __shfl_xor(hi, o));
+    }
+    uint64_t seed = 0ull;
+    if (x >= lo && x <= hi && x < V)
+        for (int k = 0; k < nb; ++k)
+            if (__builtin_amdgcn_readlane(mine, k) == x) seed |= 1ull << k;
+    if (x < VS) {
+        uint64_t *b = pl + (size_t)batch * npl * VS + x;
+        for (int p = 0; p < npl; ++p)
+            b[(size_t)p * VS] = (p == kPlVis || p == kPlFront) ? seed : 0ull;
+    }
+    if (batch == 0 && blockIdx.x == 0) {
+        for (int i = threadIdx.x; i < nflags; i += blockDim.x) flags[i] = 0;
+        __syncthreads();
+        // a last batch of one destination has its (batch, d) word complete
+        if (threadIdx.x == 0 && ndst - ((ndst - 1) & ~63) == 1) {
+            const int d = dst[ndst - 1];
+            if (d >= 0 && d < V) status[0] = 1;
+        }
+    }
+}
+
 // A busy level is a chain of dependent L2 round trips per thread -- visited
 // word, row, frontier gathers, then a read-modify-write of the level / slot
 // planes.  opt kPlAtomicOr: the plane updates are return-less atomic ORs
@@ -697,9 +737,14 @@ __global__ __launch_bounds__(256) void msbfs_plane_seed_kernel(
 // issued beside the visited load were slower on every fabric.)
 constexpr int kPlAtomicOr = 2;
 
-// status[0]: (batch, vertex) words with every destination bit set -- the BFS
-// is complete when it reaches V x batches, so no empty level is launched to
-// find out; status[1]: the last level that reached anything
+// flags[lvl]: level lvl reached something.  status[16 k], k < 16: (batch,
+// vertex) words with every destination bit set, counted over 16 words 64 B
+// apart -- the BFS is complete when their sum reaches V x batches, so no
+// empty level is launched to find out.  Both are hot words: one update per
+// wave (the flag only while it is still 0), the count spread over the 16
+// (a per-wave store and atomic on two single hot words cost the 32^3 torus
+// 12 -> 33 ms; a per-workgroup update behind a barrier 14.7 ms)
+constexpr int kStatusWords = 256;
 template <int SB>
 __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
     int V, int VS, int W, const int32_t *__restrict__ ell_col, int ndst, int lvl, int flip,
@@ -730,6 +775,8 @@ __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
 #pragma unroll
     for (int j = 0; j < WM; ++j) {
         if (j < W) {
+            // [vertex][slot] rows: a transposed u16 copy (coalesced along x)
+            // measured slower, k=48 0.110 -> 0.112 ms, dragonfly 0.104 -> 0.111
             const int n = r[j];
             f[j] = n >= 0 ? front[n] : 0ull;
         }
@@ -750,9 +797,12 @@ __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
     const uint64_t nw = (~vx & all) & ~rem;    // bits reached at this level
     next[x] = nw;
     {
-        const uint64_t fm = __ballot(nw != 0ull && ((vx | nw) & all) == all);
         const uint64_t act = __ballot(true);
-        if (fm && lane_id() == __builtin_ctzll(act)) atomicAdd(&status[0], __popcll(fm));
+        const uint64_t fm = __ballot(nw != 0ull && rem == 0ull), am = __ballot(nw != 0ull);
+        if (lane_id() == __builtin_ctzll(act)) {
+            if (fm) atomicAdd(&status[16 * (blockIdx.x & 15)], __popcll(fm));
+            if (am && changed[lvl] == 0) changed[lvl] = 1;   // racing writers all store 1
+        }
     }
     if (nw) {
         b[(size_t)kPlVis * VS + x] = vx | nw;
@@ -772,8 +822,6 @@ __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
             for (int k = 0; k < SB; ++k)
                 if (sp[k]) b[(size_t)(kPlSlot + k) * VS + x] |= sp[k];
         }
-        changed[lvl] = 1;
-        status[1] = lvl;                         // levels run in order: the last write wins
     }
 }
 
@@ -786,8 +834,28 @@ template <int SB>
 __global__ __launch_bounds__(256) void msbfs_plane_tables_kernel(
     int V, int VS, int W, const int32_t *__restrict__ ell_col, const int32_t *__restrict__ ell_port,
     int ndst, const uint64_t *__restrict__ pl, uint16_t *__restrict__ dist,
-    int32_t *__restrict__ nh, int32_t *__restrict__ nh_port)
+    int32_t *__restrict__ nh, int32_t *__restrict__ nh_port, const int *__restrict__ status,
+    int *hpub, int seq)
 {
+    // the levels before this launch are done (stream order): hand the host
+    // (coherent host memory, system scope) the complete-word count and the
+    // last level that reached anything (the highest set level flag), then
+    // the sequence number -- no copy on the stream between levels and tables
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) {
+        const int *flags = status - 256;
+        int last = 0, done = threadIdx.x < 16 ? status[16 * threadIdx.x] : 0;
+        for (int l = threadIdx.x; l < 256; l += 64)
+            if (l > 0 && flags[l]) last = l;
+        for (int o = 32; o > 0; o >>= 1) {
+            last = max(last, __shfl_xor(last, o));
+            done += __shfl_xor(done, o);
+        }
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(&hpub[0], done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&hpub[1], last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&hpub[3], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
     // [2][W][kTabStride]: ids, ports; the odd stride keeps the transposing
     // stores below conflict-free (with 256, a wave's 64 stores -- slots j,
     // j+1, ... of one or two vertices -- fell in one or two banks)
@@ -903,13 +971,14 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
     // equal chunks: a short last chunk costs a whole level sequence
     const int nchunk = (nbatch + cb - 1) / cb;
     cb = (nbatch + nchunk - 1) / nchunk;
-    int rc = sdnr_reserve(&ctx->scratch, &ctx->scratch_bytes, (size_t)cb * per_batch + 2048);
+    constexpr int kFlagInts = 256 + kStatusWords;   // level flags + 16 spread counters
+    int rc = sdnr_reserve(&ctx->scratch, &ctx->scratch_bytes,
+                          (size_t)cb * per_batch + kFlagInts * sizeof(int) + 256);
     if (rc) return rc;
     uint64_t *pl = static_cast<uint64_t *>(ctx->scratch);
     int *changed = reinterpret_cast<int *>(reinterpret_cast<char *>(ctx->scratch) +
                                            (size_t)cb * per_batch);   // [256] per level
-    int *status = changed + 256;                 // [0] complete words [1] last busy level
-    constexpr int kFlagInts = 258;
+    int *status = changed + 256;                 // complete-word counters (16, 64 B apart)
     const int gx = (V + 255) / 256;
     // level-pass options: kPlAtomicOr up to 16k vertices (k=48, dragonfly);
     // SDNROUTE_PLANE_OPT=0|2 overrides
@@ -927,6 +996,9 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
     const char *gq = getenv("SDNROUTE_PLANE_GUESS");   // 0: check every kGroup levels
     const bool noguess = gq && !strcmp(gq, "0");
     int guess = noguess ? 0 : ctx->plane_depth;
+    // SDNROUTE_PLANE_INIT=0: fills + seed kernel instead of the init kernel
+    const char *iq = getenv("SDNROUTE_PLANE_INIT");
+    const bool oldinit = iq && !strcmp(iq, "0");
     const size_t tl = d_nh ? (size_t)2 * W * 257 * sizeof(int32_t) : 0;   // kTabStride
     if (sb == 5 && tl > 65536)   // W = 32 with the padded stride
         sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<5>), tl);
@@ -937,12 +1009,18 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
         // a full chunk's planes end where the level flags begin: one fill
         // for both (one launch fewer per chunk)
         const bool full = nbc == cb;
-        SDNR_HIP(hipMemsetAsync(pl, 0, (size_t)nbc * per_batch + (full ? kFlagInts * sizeof(int) : 0),
-                                ctx->stream));
-        if (!full) SDNR_HIP(hipMemsetAsync(changed, 0, kFlagInts * sizeof(int), ctx->stream));
-        hipLaunchKernelGGL(msbfs_plane_seed_kernel, dim3((nd + 255) / 256), dim3(256), 0,
-                           ctx->stream, V, VS, d_dst + (size_t)c0 * 64, nd, pl, plane_count(sb),
-                           status);
+        if (oldinit) {
+            SDNR_HIP(hipMemsetAsync(pl, 0, (size_t)nbc * per_batch + (full ? kFlagInts * sizeof(int) : 0),
+                                    ctx->stream));
+            if (!full) SDNR_HIP(hipMemsetAsync(changed, 0, kFlagInts * sizeof(int), ctx->stream));
+            hipLaunchKernelGGL(msbfs_plane_seed_kernel, dim3((nd + 255) / 256), dim3(256), 0,
+                               ctx->stream, V, VS, d_dst + (size_t)c0 * 64, nd, pl, plane_count(sb),
+                               status);
+        } else {
+            hipLaunchKernelGGL(msbfs_plane_init_kernel, dim3((VS + 255) / 256, nbc), dim3(256), 0,
+                               ctx->stream, V, VS, d_dst + (size_t)c0 * 64, nd, pl, plane_count(sb),
+                               changed, kFlagInts, status);
+        }
         SDNR_HIP(hipGetLastError());
         uint16_t *dist = d_dist + (size_t)c0 * 64 * V;
         int32_t *nh = d_nh ? d_nh + (size_t)c0 * 64 * V : nullptr;
@@ -955,46 +1033,39 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
             upto = lvl <= guess ? guess : lvl + kGroup - 1;
             if (upto > 255) upto = 255;
             for (; lvl <= upto; ++lvl) {
-                if (sb == 3)
-                    hipLaunchKernelGGL(msbfs_plane_level_kernel<3>, dim3(gx, nbc), dim3(256), 0,
-                                       ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1,
-                                       pl, changed, popt, status);
-                else if (sb == 4)
-                    hipLaunchKernelGGL(msbfs_plane_level_kernel<4>, dim3(gx, nbc), dim3(256), 0,
-                                       ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1,
-                                       pl, changed, popt, status);
-                else if (sb == 5)
-                    hipLaunchKernelGGL(msbfs_plane_level_kernel<5>, dim3(gx, nbc), dim3(256), 0,
-                                       ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1,
-                                       pl, changed, popt, status);
-                else
-                    hipLaunchKernelGGL(msbfs_plane_level_kernel<6>, dim3(gx, nbc), dim3(256), 0,
-                                       ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1,
-                                       pl, changed, popt, status);
+#define SDNR_LEVEL(SB_)                                                                       \
+    hipLaunchKernelGGL(msbfs_plane_level_kernel<SB_>, dim3(gx, nbc), dim3(256), 0, ctx->stream, \
+                       V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl, changed, popt, status)
+                if (sb == 3) SDNR_LEVEL(3);
+                else if (sb == 4) SDNR_LEVEL(4);
+                else if (sb == 5) SDNR_LEVEL(5);
+                else SDNR_LEVEL(6);
+#undef SDNR_LEVEL
                 SDNR_HIP(hipGetLastError());
             }
-            // the check's copy goes on the stream BEHIND the levels and AHEAD of
-            // the table pass: the host waits for the levels only, and returns
-            // while the table pass runs (the next call's launches overlap it)
-            if ((rc = sdnr_fetch_ints_begin(ctx, status, 2))) return rc;
+            // the table pass publishes the levels' status to the host as it
+            // starts: the host waits for the levels only, and returns while
+            // the table pass runs (the next call's launches overlap it)
+            const int seq = ++ctx->pub_seq;
+            int *hp = ctx->h_pub;
             if (sb == 3)
                 hipLaunchKernelGGL(msbfs_plane_tables_kernel<3>, dim3(gx, nbc), dim3(256), tl,
                                    ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist,
-                                   nh, nhp);
+                                   nh, nhp, status, hp, seq);
             else if (sb == 4)
                 hipLaunchKernelGGL(msbfs_plane_tables_kernel<4>, dim3(gx, nbc), dim3(256), tl,
                                    ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist,
-                                   nh, nhp);
+                                   nh, nhp, status, hp, seq);
             else if (sb == 5)
                 hipLaunchKernelGGL(msbfs_plane_tables_kernel<5>, dim3(gx, nbc), dim3(256), tl,
                                    ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist,
-                                   nh, nhp);
+                                   nh, nhp, status, hp, seq);
             else
                 hipLaunchKernelGGL(msbfs_plane_tables_kernel<6>, dim3(gx, nbc), dim3(256), tl,
                                    ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist,
-                                   nh, nhp);
+                                   nh, nhp, status, hp, seq);
             SDNR_HIP(hipGetLastError());
-            if ((rc = sdnr_fetch_ints_end(ctx, 2, st))) return rc;
+            if ((rc = sdnr_wait_published(ctx, seq, 2, st))) return rc;
             if ((long long)st[0] == target || st[1] < upto) break;
             if (upto == 255) return 1;           // deeper than 255 levels
         }

@@ -95,7 +95,13 @@ def _bind(L):
         "sdnr_last_sweeps": ([vp, ctypes.POINTER(i32)], c_int),
         "sdnr_edge_ports": ([vp, vp, i32, vp, i32, vp, u32], c_int),
     }
+    # an A/B build named by SDNROUTE_LIB may predate some entry points: those
+    # stay unbound (calling one raises AttributeError); the in-tree library
+    # must export every one
+    older_ok = "SDNROUTE_LIB" in os.environ
     for name, (args, res) in sig.items():
+        if older_ok and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
