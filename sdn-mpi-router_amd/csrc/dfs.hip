@@ -1506,7 +1506,13 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int swz(int x) { return lds_swz(x); }   // common.h
 
-template <int NW, bool HOPS, bool PACKED, bool C16, bool PAIR>
+// PAIR: how a worker loads the pre-swizzled in-rows -- 0: one u16 row (64
+// lanes) per child; 1: rows of <= 32 entries repeated in lanes 32..63, one
+// load for two children; 2: the 64-entry rows read as 32 u32 words, lanes
+// 0..31 child 2g and 32..63 child 2g + 1, two ds_sub per lane -- half the
+// load instructions and half the returned dwords of PAIR 0 (the CU's
+// vector-memory data return is 71 % busy at the k=48 headline's load)
+template <int NW, bool HOPS, bool PACKED, bool C16, int PAIR>
 __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
     int V, const uint16_t *__restrict__ adj, const uint16_t *__restrict__ radj,
     const uint32_t *__restrict__ deg, const int32_t *__restrict__ row_ptr,
@@ -1828,7 +1834,28 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                 spin = 0;
                 const int n = (P - j + S - 1) / S < G ? (P - j + S - 1) / S : G;
                 const int mine = lane < n ? (int)ring[(j + lane * S) & (RING - 1)] : V;
-                if constexpr (PAIR) {
+                if constexpr (PAIR == 2) {
+                    constexpr int G2 = G / 2;
+                    const int hiw = lane >> 5;
+                    const uint32_t *rw32 = reinterpret_cast<const uint32_t *>(radj);
+                    uint32_t r[G2];
+#pragma unroll
+                    for (int g = 0; g < G2; ++g) {
+                        const int ca = read_lane(mine, 2 * g), cb = read_lane(mine, 2 * g + 1);
+                        r[g] = rw32[(size_t)(hiw ? cb : ca) * 32 + (lane & 31)];
+                    }
+#pragma unroll
+                    for (int g = 0; g < G2; ++g)
+                        if (2 * g + hiw < n) {
+                            atomicSub(&cnt[r[g] & 0xFFFFu], 1u);
+                            atomicSub(&cnt[r[g] >> 16], 1u);
+                        }
+                    j += n * S;
+                    if (lane == 0) __hip_atomic_store(&ctl[2 + w - 1], j, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                    continue;
+                }
+                if constexpr (PAIR == 1) {
                     // rows repeat in lanes 32..63: load g serves child 2g in
                     // lanes 0..31 and child 2g + 1 in lanes 32..63 (a template
                     // case: a runtime branch here cost the unpaired k=48
@@ -2513,8 +2540,15 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         const uint16_t *rw = c16 ? ctx->radjc : ctx->radjw;
         const bool preswz = rw && !(pz && !strcmp(pz, "0"));
         const int aflags = dfs_flags(kFlagPrio) | (preswz ? kFlagPreSwz : 0) | hflags;
-        // paired worker rows (in-degree <= 32, pre-swizzled rows only)
+        // paired worker rows (in-degree <= 32, pre-swizzled rows only);
+        // else, at <= 2 sources per CU (the 5-worker regime), dword-paired
+        // rows: k=48 1 / 144 sources 56.3 / 57.8 -> 54.7 / 56.4 us; at the
+        // 1,152-source headline they measured 0.0895 -> 0.1010 ms, so the
+        // u16 rows stay there (SDNROUTE_DFS_DW=0|1 forces either)
         const bool pair = preswz && ctx->radj_pair;
+        const char *dq = getenv("SDNROUTE_DFS_DW");
+        bool dw = preswz && !pair && !c16 && nw == 6;
+        if (dq) dw = preswz && !pair && !c16 && !strcmp(dq, "1");
         int cgrid = (int)((size_t)ctx->num_cus * cpc);
         if (cgrid > nsrc) cgrid = nsrc;
         // the search wave issues at raised priority over the decrement
@@ -2525,10 +2559,11 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         ctx->last_kernel = names[nw];
 #define SDNR_ASYNC_P(N_, H_, P_)                                                             \
     do {                                                                                     \
-        auto k = c16 ? (pair ? dfs_async_kernel<N_, H_, P_, true, true>                      \
-                             : dfs_async_kernel<N_, H_, P_, true, false>)                    \
-                     : (pair ? dfs_async_kernel<N_, H_, P_, false, true>                     \
-                             : dfs_async_kernel<N_, H_, P_, false, false>);                  \
+        auto k = c16 ? (pair ? dfs_async_kernel<N_, H_, P_, true, 1>                         \
+                             : dfs_async_kernel<N_, H_, P_, true, 0>)                        \
+                     : (pair ? dfs_async_kernel<N_, H_, P_, false, 1>                        \
+                             : (dw ? dfs_async_kernel<N_, H_, P_, false, 2>                  \
+                                   : dfs_async_kernel<N_, H_, P_, false, 0>));               \
         allow_full_lds(k);                                                                   \
         hipLaunchKernelGGL(k, dim3(cgrid), dim3(N_ * 64), cl, ctx->stream, V, ctx->adj16,    \
                            preswz ? rw : ctx->radj16, ctx->deg32, ctx->row_ptr,              \

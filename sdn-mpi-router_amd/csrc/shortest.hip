@@ -830,7 +830,7 @@ __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
 // once, transposed to [slot][vertex] so the per-destination lookups of a
 // wave hit 32 different banks, instead of two scattered global loads per
 // (destination, vertex)
-template <int SB>
+template <int SB, int TB, int Q>
 __global__ __launch_bounds__(256) void msbfs_plane_tables_kernel(
     int V, int VS, int W, const int32_t *__restrict__ ell_col, const int32_t *__restrict__ ell_port,
     int ndst, const uint64_t *__restrict__ pl, uint16_t *__restrict__ dist,
@@ -858,16 +858,22 @@ __global__ __launch_bounds__(256) void msbfs_plane_tables_kernel(
     }
     // [2][W][kTabStride]: ids, ports; the odd stride keeps the transposing
     // stores below conflict-free (with 256, a wave's 64 stores -- slots j,
-    // j+1, ... of one or two vertices -- fell in one or two banks)
-    constexpr int kTabStride = 257;
+    // j+1, ... of one or two vertices -- fell in one or two banks).  TB
+    // vertices per block, each decoded by Q threads (64 / Q destinations
+    // each): the decode is ~3.5 k VALU instructions per wave for 64
+    // destinations, so on small graphs (k=48: 12 x 18 blocks of 256 for 256
+    // CUs, one wave per SIMD) 64-vertex blocks with Q = 4 give each SIMD
+    // several waves to hide that latency, with no extra row staging
+    constexpr int kTabStride = TB + 1;
     extern __shared__ int32_t lrow[];
-    const int x0 = blockIdx.x * blockDim.x;
-    const int t = threadIdx.x;
+    const int x0 = blockIdx.x * TB;
+    const int t = threadIdx.x % TB;
+    const int q = threadIdx.x / TB;
     const int x = x0 + t;
     const int batch = blockIdx.y;
-    const int nx = min(256, V - x0);
+    const int nx = min(TB, V - x0);
     if (nh) {
-        for (int e = t; e < nx * W; e += 256) {   // coalesced reads of the block's rows
+        for (int e = threadIdx.x; e < nx * W; e += TB * Q) {   // coalesced reads of the rows
             const int xl = e / W, j = e - xl * W;
             lrow[j * kTabStride + xl] = ell_col[(size_t)x0 * W + e];
             lrow[(W + j) * kTabStride + xl] = ell_port[(size_t)x0 * W + e];
@@ -887,7 +893,8 @@ __global__ __launch_bounds__(256) void msbfs_plane_tables_kernel(
     // bit extracts after that), the group's 16 LDS lookups issued together
     // before its stores, instead of one dependent lookup per destination
     constexpr int CG = 8;
-    for (int i0 = 0; i0 < nb; i0 += CG) {
+    const int iend = min(nb, (q + 1) * (64 / Q));
+    for (int i0 = q * (64 / Q); i0 < iend; i0 += CG) {
         const uint32_t vv = (uint32_t)(vx >> i0);
         uint32_t dv[8], sv[SB];
 #pragma unroll
@@ -917,7 +924,7 @@ __global__ __launch_bounds__(256) void msbfs_plane_tables_kernel(
         }
 #pragma unroll
         for (int u = 0; u < CG; ++u) {
-            if (i0 + u < nb) {
+            if (i0 + u < iend) {
                 const size_t row = (size_t)(batch * 64 + i0 + u) * V + x;
                 dist[row] = (uint16_t)L[u];
                 if (nh) {
@@ -999,10 +1006,16 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
     // SDNROUTE_PLANE_INIT=0: fills + seed kernel instead of the init kernel
     const char *iq = getenv("SDNROUTE_PLANE_INIT");
     const bool oldinit = iq && !strcmp(iq, "0");
-    const size_t tl = d_nh ? (size_t)2 * W * 257 * sizeof(int32_t) : 0;   // kTabStride
+    const size_t tl = d_nh ? (size_t)2 * W * 257 * sizeof(int32_t) : 0;   // kTabStride, TB 256
     if (sb == 5 && tl > 65536)   // W = 32 with the padded stride
-        sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<5>), tl);
-    if (sb == 6) sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<6>), tl);
+        sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<5, 256, 1>), tl);
+    if (sb == 6) sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<6, 256, 1>), tl);
+    // small launches (fewer 256-vertex blocks than 2 per CU over the whole
+    // destination set): 64-vertex blocks, so every CU gets work
+    // (SDNROUTE_PLANE_BLOCK=256|64 overrides)
+    bool small = (size_t)gx * nbatch < 2 * (size_t)ctx->num_cus;
+    if (const char *f = getenv("SDNROUTE_PLANE_BLOCK")) small = atoi(f) == 64;
+    const int lb = small ? 64 : 256;
     for (int c0 = 0; c0 < nbatch; c0 += cb) {
         const int nbc = nbatch - c0 < cb ? nbatch - c0 : cb;
         const int nd = ndst - c0 * 64 < nbc * 64 ? ndst - c0 * 64 : nbc * 64;
@@ -1034,8 +1047,9 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
             if (upto > 255) upto = 255;
             for (; lvl <= upto; ++lvl) {
 #define SDNR_LEVEL(SB_)                                                                       \
-    hipLaunchKernelGGL(msbfs_plane_level_kernel<SB_>, dim3(gx, nbc), dim3(256), 0, ctx->stream, \
-                       V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl, changed, popt, status)
+    hipLaunchKernelGGL(msbfs_plane_level_kernel<SB_>, dim3((V + lb - 1) / lb, nbc), dim3(lb), 0,  \
+                       ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl, changed,  \
+                       popt, status)
                 if (sb == 3) SDNR_LEVEL(3);
                 else if (sb == 4) SDNR_LEVEL(4);
                 else if (sb == 5) SDNR_LEVEL(5);
@@ -1048,22 +1062,22 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
             // the table pass runs (the next call's launches overlap it)
             const int seq = ++ctx->pub_seq;
             int *hp = ctx->h_pub;
-            if (sb == 3)
-                hipLaunchKernelGGL(msbfs_plane_tables_kernel<3>, dim3(gx, nbc), dim3(256), tl,
-                                   ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist,
-                                   nh, nhp, status, hp, seq);
-            else if (sb == 4)
-                hipLaunchKernelGGL(msbfs_plane_tables_kernel<4>, dim3(gx, nbc), dim3(256), tl,
-                                   ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist,
-                                   nh, nhp, status, hp, seq);
-            else if (sb == 5)
-                hipLaunchKernelGGL(msbfs_plane_tables_kernel<5>, dim3(gx, nbc), dim3(256), tl,
-                                   ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist,
-                                   nh, nhp, status, hp, seq);
-            else
-                hipLaunchKernelGGL(msbfs_plane_tables_kernel<6>, dim3(gx, nbc), dim3(256), tl,
-                                   ctx->stream, V, VS, W, ctx->ell_col, ctx->ell_port, nd, pl, dist,
-                                   nh, nhp, status, hp, seq);
+#define SDNR_TABLES(SB_, TB_, Q_)                                                               \
+    hipLaunchKernelGGL((msbfs_plane_tables_kernel<SB_, TB_, Q_>), dim3((V + TB_ - 1) / TB_, nbc), \
+                       dim3(TB_ * Q_), (size_t)(nh ? 2 * W * (TB_ + 1) * 4 : 0), ctx->stream, V, VS, \
+                       W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh, nhp, status, hp, seq)
+            if (small) {
+                if (sb == 3) SDNR_TABLES(3, 64, 4);
+                else if (sb == 4) SDNR_TABLES(4, 64, 4);
+                else if (sb == 5) SDNR_TABLES(5, 64, 4);
+                else SDNR_TABLES(6, 64, 4);
+            } else {
+                if (sb == 3) SDNR_TABLES(3, 256, 1);
+                else if (sb == 4) SDNR_TABLES(4, 256, 1);
+                else if (sb == 5) SDNR_TABLES(5, 256, 1);
+                else SDNR_TABLES(6, 256, 1);
+            }
+#undef SDNR_TABLES
             SDNR_HIP(hipGetLastError());
             if ((rc = sdnr_wait_published(ctx, seq, 2, st))) return rc;
             if ((long long)st[0] == target || st[1] < upto) break;
