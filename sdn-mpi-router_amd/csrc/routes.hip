@@ -265,8 +265,10 @@ __device__ __forceinline__ int wave_incl_scan(int x)
 // to one per distinct path entry.  A pair whose path alone exceeds CAP is
 // walked straight to global memory (16 lanes, as the jump kernel).
 // OUTP: entries as one u32 each, switch | port << 16 (the tree word layout:
-// the LDS buffer is copied as is) instead of two int32 arrays
-template <int CAP, bool NT, bool OUTP>
+// the LDS buffer is copied as is) instead of two int32 arrays.  V4: a run's
+// entries go out as 16-B stores, 4 consecutive entries per lane (per array),
+// after a head of up to 3 single entries to the 16-B boundary
+template <int CAP, bool NT, bool OUTP, bool V4 = false>
 __global__ __launch_bounds__(256) void route_seg_packed_kernel(
     int V, const uint32_t *__restrict__ tree, Anc16 anc,
     const int32_t *__restrict__ rows, const int32_t *__restrict__ dsts,
@@ -389,6 +391,77 @@ __global__ __launch_bounds__(256) void route_seg_packed_kernel(
                 const int sop = read_lane(segoff, p0), dp = read_lane(d, p0);
                 const int total = (p1 - p0) * Lr;
                 const float inv = 1.0f / (float)Lr;
+                // (a run shorter than one 16-B pass -- random pairs, one pair
+                // per run -- keeps the 4-B stores: head + body + tail would be
+                // three partly empty store passes; 1,024-rank flows measured
+                // 0.48 -> 0.61 ms with 16-B stores everywhere)
+                if (V4 && total >= 256) {
+                    // entry at flat index t of the run: pair q = t / Lr, hop k
+                    auto qk = [&](int t, int &q, int &k) {
+                        q = (int)((float)t * inv);
+                        k = t - q * Lr;
+                        if (k >= Lr) { ++q; k -= Lr; }
+                        if (k < 0) { --q; k += Lr; }
+                    };
+                    auto word = [&](int q, int k) -> uint32_t {
+                        return k < Lr - 1 ? buf[sop + k] : (uint32_t)dp | ((uint32_t)lps[p0 + q] << 16);
+                    };
+                    // u32 entries, or the switch / port int32 arrays (same
+                    // offsets, so one alignment for both)
+                    uint32_t *o = reinterpret_cast<uint32_t *>(hop_switch) + lop;
+                    uint32_t *op = OUTP ? nullptr : reinterpret_cast<uint32_t *>(hop_port) + lop;
+                    // int32 form: switch and port of entry (q, k); the last
+                    // entry's port is the request's, any int32
+                    auto sw_of = [&](int k) -> uint32_t {
+                        return k < Lr - 1 ? (buf[sop + k] & 0xFFFFu) : (uint32_t)dp;
+                    };
+                    auto pt_of = [&](int q, int k) -> uint32_t {
+                        return k < Lr - 1 ? (buf[sop + k] >> 16) : (uint32_t)lps[p0 + q];
+                    };
+                    auto put1 = [&](int t, int q, int k) {
+                        if (OUTP) {
+                            o[t] = word(q, k);
+                        } else {
+                            o[t] = sw_of(k);
+                            op[t] = pt_of(q, k);
+                        }
+                    };
+                    const int head = min(total, (int)(((16u - ((uint32_t)(uintptr_t)o & 15u)) & 15u) >> 2));
+                    if (lane < head) {
+                        int q, k;
+                        qk(lane, q, k);
+                        put1(lane, q, k);
+                    }
+                    const int bend = head + ((total - head) & ~3);
+                    for (int t0 = head; t0 < bend; t0 += 256) {
+                        const int t = t0 + 4 * lane;
+                        if (t < bend) {
+                            int q, k;
+                            qk(t, q, k);
+                            uint32_t a[4], b[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                if (OUTP) {
+                                    a[u] = word(q, k);
+                                } else {
+                                    a[u] = sw_of(k);
+                                    b[u] = pt_of(q, k);
+                                }
+                                if (++k == Lr) { k = 0; ++q; }
+                            }
+                            // 16-B aligned (o and op share the offset)
+                            *reinterpret_cast<uint4 *>(o + t) = make_uint4(a[0], a[1], a[2], a[3]);
+                            if (!OUTP)
+                                *reinterpret_cast<uint4 *>(op + t) = make_uint4(b[0], b[1], b[2], b[3]);
+                        }
+                    }
+                    if (bend + lane < total) {
+                        int q, k;
+                        qk(bend + lane, q, k);
+                        put1(bend + lane, q, k);
+                    }
+                    continue;
+                }
                 for (int t0 = 0; t0 < total; t0 += 64) {
                     const int t = t0 + lane;
                     if (t < total) {
@@ -545,18 +618,32 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
             int64_t g = (((int64_t)npairs + 63) / 64 + 3) / 4;
             if (g > ctx->num_cus * 8) g = ctx->num_cus * 8;
             const char *nt = getenv("SDNROUTE_ROUTE_NT");       // "1": non-temporal stores
+            // 16-B stores of 4 entries per lane (SDNROUTE_ROUTE_V4=0: 4-B stores)
+            const char *v4 = getenv("SDNROUTE_ROUTE_V4");
             if (d_entries) {
                 ctx->last_kernel = "route_seg_packed_kernel<1024,u32>";
-                hipLaunchKernelGGL((route_seg_packed_kernel<1024, false, true>), dim3((unsigned)g),
-                                   dim3(256), 0, ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts,
-                                   d_last_port, npairs, d_off, reinterpret_cast<int32_t *>(d_entries),
-                                   nullptr);
+                if (v4 && !strcmp(v4, "0"))
+                    hipLaunchKernelGGL((route_seg_packed_kernel<1024, false, true, false>),
+                                       dim3((unsigned)g), dim3(256), 0, ctx->stream, ctx->V, tree,
+                                       tabs, d_rows, d_dsts, d_last_port, npairs, d_off,
+                                       reinterpret_cast<int32_t *>(d_entries), nullptr);
+                else
+                    hipLaunchKernelGGL((route_seg_packed_kernel<1024, false, true, true>),
+                                       dim3((unsigned)g), dim3(256), 0, ctx->stream, ctx->V, tree,
+                                       tabs, d_rows, d_dsts, d_last_port, npairs, d_off,
+                                       reinterpret_cast<int32_t *>(d_entries), nullptr);
             } else {
                 ctx->last_kernel = "route_seg_packed_kernel<1024>";
                 if (nt && !strcmp(nt, "1"))
                     hipLaunchKernelGGL((route_seg_packed_kernel<1024, true, false>), dim3((unsigned)g),
                                        dim3(256), 0, ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts,
                                        d_last_port, npairs, d_off, d_switch, d_hport);
+                else if ((((uintptr_t)d_switch ^ (uintptr_t)d_hport) & 15u) == 0 && !(v4 && !strcmp(v4, "0")))
+                    // both arrays share their 16-B phase: 16-B stores into each
+                    hipLaunchKernelGGL((route_seg_packed_kernel<1024, false, false, true>),
+                                       dim3((unsigned)g), dim3(256), 0, ctx->stream, ctx->V, tree,
+                                       tabs, d_rows, d_dsts, d_last_port, npairs, d_off, d_switch,
+                                       d_hport);
                 else
                     hipLaunchKernelGGL((route_seg_packed_kernel<1024, false, false>), dim3((unsigned)g),
                                        dim3(256), 0, ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts,

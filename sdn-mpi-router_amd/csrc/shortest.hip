@@ -1030,7 +1030,7 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
                                ctx->stream, V, VS, d_dst + (size_t)c0 * 64, nd, pl, plane_count(sb),
                                status);
         } else {
-            hipLaunchKernelGGL(msbfs_plane_init_kernel, dim3((VS + 255) / 256, nbc), dim3(256), 0,
+            hipLaunchKernelGGL(msbfs_plane_init_kernel, dim3((VS + lb - 1) / lb, nbc), dim3(lb), 0,
                                ctx->stream, V, VS, d_dst + (size_t)c0 * 64, nd, pl, plane_count(sb),
                                changed, kFlagInts, status);
         }

@@ -320,7 +320,8 @@ def test_route_entries_batched_fake_engine():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("walk", ["auto", "seg32", "jump16", "serial", "int32", "p4", "p8"])
+@pytest.mark.parametrize("walk", ["auto", "seg32", "v1", "v1seg32", "jump16", "serial", "int32",
+                                  "p4", "p8"])
 @pytest.mark.parametrize("name", ["mock", "fat_tree_k8", "dragonfly_a4_h2_p2", "random_V40",
                                   "torus_5x3x2"])
 def test_route_entries_match_reference(monkeypatch, name, walk):
@@ -333,6 +334,10 @@ def test_route_entries_match_reference(monkeypatch, name, walk):
         monkeypatch.setenv("SDNROUTE_ROUTE_SEG", "0")
     elif walk == "seg32":                        # entries as two int32 arrays
         monkeypatch.setenv("SDNROUTE_ROUTE_OUT", "int32")
+    elif walk.startswith("v1"):                  # 4-B stores instead of 16-B ones
+        monkeypatch.setenv("SDNROUTE_ROUTE_V4", "0")
+        if walk == "v1seg32":
+            monkeypatch.setenv("SDNROUTE_ROUTE_OUT", "int32")
     elif walk != "auto":                         # int32-table jump kernels
         monkeypatch.setenv("SDNROUTE_ROUTE_PACKED", "0")
         if walk != "int32":
@@ -415,6 +420,14 @@ def test_route_entries_runs_and_long_paths(monkeypatch, fab):
     assert db.engine.ctx.last_kernel() == "route_seg_packed_kernel<1024>"
     for a, b in ((o1, o2), (d1, d2), (p1, p2)):
         np.testing.assert_array_equal(a, b)
+    monkeypatch.setenv("SDNROUTE_ROUTE_V4", "0")         # 4-B stores, both forms
+    for out in ("int32", "u32"):
+        monkeypatch.setenv("SDNROUTE_ROUTE_OUT", out)
+        o3, d3, p3 = db.route_entries(pairs)
+        for a, b in ((o1, o3), (d1, d3), (p1, p3)):
+            np.testing.assert_array_equal(a, b)
+    monkeypatch.delenv("SDNROUTE_ROUTE_V4")
+    monkeypatch.delenv("SDNROUTE_ROUTE_OUT")
     if not fab.startswith("fat"):
         assert int(np.diff(o0).max()) > 1024     # some pairs take the direct walk
     np.testing.assert_array_equal(o0, o1)

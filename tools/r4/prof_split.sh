@@ -6,7 +6,7 @@ set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/r4_split; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-GROUPS=("VmemLatency" "LdsLatency"
+CGROUPS=("VmemLatency" "LdsLatency"
         "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_PENDING_STALL_CYCLES_sum"
         "TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum"
         "SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INST_CYCLES_SALU SQ_BUSY_CYCLES"
@@ -14,7 +14,7 @@ GROUPS=("VmemLatency" "LdsLatency"
 run() {  # tag, bench args...
   local tag=$1; shift
   local i=0
-  for g in "${GROUPS[@]}"; do
+  for g in "${CGROUPS[@]}"; do
     i=$((i+1))
     timeout -s KILL 300 rocprofv3 --pmc $g -f csv -d $OUT/$tag/p$i -o run -- \
       python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-flows "$@" > $OUT/$tag/p$i.log 2>&1
