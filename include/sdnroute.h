@@ -228,10 +228,15 @@ int sdnr_route_expand(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port,
                       const int64_t *offsets, int32_t *hop_switch,
                       int32_t *hop_port, uint32_t flags);
 
-/* The same entries as ONE u32 word each, switch | out_port << 16 (the
+/* Replaces, like sdnr_route_expand, _route_to_fdb for many pairs
+ * (sdnmpi/util/topology_db.py:127-138; the entries Router._add_flows_for_path
+ * installs, sdnmpi/router.py:83-104).
+ * The same entries as ONE u32 word each, switch | out_port << 16 (the
  * packed tree word's layout: a dense switch id and a 16-bit OpenFlow 1.0
  * port, OFPP_LOCAL = 0xfffe included) -- half the bytes of the two int32
- * arrays.  Needs V <= 65535, 16-bit ports and last ports <= 0xffff; device
+ * arrays.  Needs V <= 65535 and 16-bit link ports (else SDNR_ERR_INVAL);
+ * a last (host) port above 0xffff keeps only its low 16 bits, so callers
+ * with such ports use sdnr_route_expand (the drop-in does).  Device
  * pointers only (flags must hold SDNR_DEVICE_PTRS). */
 int sdnr_route_expand_packed(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port,
                              int32_t nrows, const int32_t *rows, const int32_t *dsts,
