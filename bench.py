@@ -351,8 +351,9 @@ def materialised_flows(ctx, dev, stream, csr, fabric, srcs, chunk=1 << 24, packe
             "event_ms": ms,
             "kernel": ctx.last_kernel(), "chunk_pairs": chunk,
             "entry_bytes": 4 if packed else 8,
+            "form": "u32 switch | port << 16" if packed else "int32 switch + int32 port",
             "note": "flow entries (dpid, out_port) of all %d^2 host pairs written to HBM "
-                    "(offsets + route_jump expansion per %d-pair chunk, one reused output "
+                    "(offsets + output-centric expansion per %d-pair chunk, one reused output "
                     "buffer), tables and requests resident; compare the headline, which "
                     "counts pairs whose route the tables determine" % (H, chunk)}
 
@@ -368,20 +369,20 @@ def main_matflows(args, world, rank, local, dev):
     ctx.upload(csr)
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
-    res = [materialised_flows(ctx, dev, stream, csr, fabric, srcs)
-           for _ in range(max(1, args.steps))]
-    best = min(res, key=lambda r: r["ms"])
     resp = [materialised_flows(ctx, dev, stream, csr, fabric, srcs, packed=True)
             for _ in range(max(1, args.steps))]
     bestp = min(resp, key=lambda r: r["ms"])
+    res = [materialised_flows(ctx, dev, stream, csr, fabric, srcs)
+           for _ in range(max(1, args.steps))]
+    best = min(res, key=lambda r: r["ms"])
     if rank == 0:
         print(json.dumps({"metric": "materialised flow entries of all host pairs, pairs/sec",
-                          "value": best["value"], "unit": "routes/s", "n_gpus": 1,
-                          "ms_per_step": best["ms"], "all_ms": [r["ms"] for r in res],
-                          "steps": len(res), "higher_is_better": True,
+                          "value": bestp["value"], "unit": "routes/s", "n_gpus": 1,
+                          "ms_per_step": bestp["ms"], "all_ms": [r["ms"] for r in resp],
+                          "steps": len(resp), "higher_is_better": True,
                           "config": {"workload": "%s materialised flows" % args.fabric},
-                          "materialised_flows": best, "packed_all_ms": [r["ms"] for r in resp],
-                          "materialised_flows_packed": bestp}), flush=True)
+                          "materialised_flows": bestp, "int32_all_ms": [r["ms"] for r in res],
+                          "materialised_flows_int32": best}), flush=True)
     ctx.close()
 
 
@@ -944,9 +945,11 @@ def main():
     # Jellyfish all-pairs fdb set (~2,400-5,600 entries per pair) is TBs
     if rank == 0 and world == 1 and args.mode == "dfs" and not args.max_sources and \
             not args.no_flows and args.fabric.startswith("fat_tree"):
-        out["materialised_flows"] = materialised_flows(ctx, dev, stream, csr, fabric, srcs)
-        out["materialised_flows_packed"] = materialised_flows(ctx, dev, stream, csr, fabric, srcs,
-                                                              packed=True)
+        # the form the drop-in uses: one u32 word (switch | port << 16) per
+        # entry, 4 B; the two int32 arrays (8 B per entry) beside it
+        out["materialised_flows"] = materialised_flows(ctx, dev, stream, csr, fabric, srcs,
+                                                       packed=True)
+        out["materialised_flows_int32"] = materialised_flows(ctx, dev, stream, csr, fabric, srcs)
     if rank == 0 and world == 1 and args.mode == "dfs" and not args.max_sources and \
             not args.no_flows and args.fabric.startswith("fat_tree"):
         out["dropin"] = dropin_block(fabric)

@@ -1676,6 +1676,11 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                     if (x < 0 && u == pu[k]) x = (int)xp[k];
                 if (x < 0) x = (int)adj[(size_t)u * 64 + lane];
                 const uint32_t wv = vis[x >> 5];
+                // the row's counts ride along with its visited words (one
+                // wait for both; read in every lane: x <= V is always a count
+                // word); a count read earlier is at most staler, i.e. high,
+                // which the row check absorbs
+                const uint32_t cc = cnt_of(x);
                 const bool fresh = ((wv >> (x & 31)) & 1u) == 0u;
                 const uint64_t mm = __ballot(fresh);
 #ifdef SDNR_STAMPS
@@ -1726,13 +1731,6 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
 #endif
                     __builtin_amdgcn_s_sleep(1);
                 }
-                // the children's counts are read FIRST: LDS ops complete in
-                // order, so behind the mark / stack / ring / parent writes the
-                // gather waited for all four; issued before them it returns
-                // while they drain.  Read in every lane (x <= V is always a
-                // count word): under `if (fresh)` the compiler closed the
-                // masked block with the wait, before the writes were issued
-                const uint32_t cc = cnt_of(x);
                 if (fresh) {
                     atomicOr(&vis[x >> 5], 1u << (x & 31));
                     if (C16) {

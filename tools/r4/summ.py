@@ -20,6 +20,10 @@ for f in sorted(glob.glob(os.path.join(d, "*.json"))):
         extra += " packed %.1f ms" % j["materialised_flows_packed"]["ms"]
     if "packed_all_ms" in j:
         extra += " packed_all_ms %s" % ["%.1f" % x for x in j["packed_all_ms"]]
+    if "materialised_flows_int32" in j:
+        extra += " int32 %.1f ms" % j["materialised_flows_int32"]["ms"]
+    if "int32_all_ms" in j:
+        extra += " int32_all_ms %s" % ["%.1f" % x for x in j["int32_all_ms"]]
     if "all_ms" in j:
         extra += " all_ms %s" % ["%.1f" % x for x in j["all_ms"]]
     print("%-24s ms/step %8.4f kern %8.4f frac %.3f %s%s" % (
