@@ -1679,10 +1679,19 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                 // the row's counts ride along with its visited words (one
                 // wait for both; read in every lane: x <= V is always a count
                 // word); a count read earlier is at most staler, i.e. high,
-                // which the row check absorbs
-                const uint32_t cc = cnt_of(x);
+                // which the row check absorbs -- so a plain load will do (as
+                // an atomic load it waited for this wave's earlier LDS writes)
+                uint32_t cc;
+                if constexpr (C16)
+                    cc = (cnt[swz(x >> 1)] >> ((x & 1) << 4)) & 0xFFFFu;
+                else
+                    cc = cnt[swz(x)];
                 const bool fresh = ((wv >> (x & 31)) & 1u) == 0u;
                 const uint64_t mm = __ballot(fresh);
+                // balloted here, ahead of the leaf-pop exit, so the count
+                // read stays beside the visited read (used after the exit, the
+                // compiler sank it there: a second round trip)
+                const uint64_t ccm = __ballot(cc != 0u);
 #ifdef SDNR_STAMPS
                 SDNR_STAMP(tb);
                 st_row += tb - ta;
@@ -1695,20 +1704,22 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                 if (mm == 0) return -1;          // stale count: a leaf pop after all
                 const int c = __popcll(mm);
                 const int rank = lanes_below(mm);
-                // the next candidates are most likely the newest children
-                {
-                    uint64_t rest = mm;
-#pragma unroll
-                    for (int k = 0; k < NPF; ++k) {
-                        if (rest) {
-                            const int h = highest_lane(rest);
-                            rest &= ~(1ull << h);
-                            pu[k] = read_lane(x, h);
-                            xp[k] = adj[(size_t)pu[k] * 64 + lane];
-                        } else {
-                            pu[k] = -1;
-                        }
-                    }
+                // the next candidate is known here, the counts having come
+                // with the visited words: the highest fresh child with a count
+                // (the children above it are leaves -- counts are never low --
+                // and are popped).  Its row is the one prefetched, and its
+                // stack position is a scalar popcount: one ballot -> readlane
+                // chain per candidate instead of two
+                const uint64_t mc = ccm & mm;
+                int nu = -1, below = 0;
+                if (mc) {
+                    const int hl = highest_lane(mc);
+                    nu = read_lane(x, hl);
+                    below = __popcll(mm & ((1ull << hl) - 1ull));   // fresh children under it
+                    pu[0] = nu;
+                    xp[0] = adj[(size_t)nu * 64 + lane];
+                } else {
+                    pu[0] = -1;                  // the next candidate comes off the stack
                 }
                 int du = 0;
                 if (HOPS) du = uniform((int)dep[u]);
@@ -1752,16 +1763,8 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                 __asm__ volatile("" ::: "memory");
                 if (lane == 0) __hip_atomic_store(&ctl[0], pub, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-                const uint64_t mc = __ballot(cc != 0u) & mm;     // fresh children with a count
                 pubd = pub;
-                int nu = -1;
-                if (mc) {
-                    // children above the highest one with a count are leaves
-                    // (counts are never low): popped; it is the next candidate
-                    const int hl = highest_lane(mc);
-                    nu = read_lane(x, hl);
-                    sp += read_lane(rank, hl);
-                }
+                sp += below;
 #ifdef SDNR_STAMPS
                 SDNR_STAMP(st_tc);
                 st_pushc += st_tc - tb;

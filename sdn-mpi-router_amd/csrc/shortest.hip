@@ -747,11 +747,15 @@ constexpr int kPlAtomicOr = 2;
 constexpr int kStatusWords = 256;
 template <int SB>
 __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
-    int V, int VS, int W, const int32_t *__restrict__ ell_col, int ndst, int lvl, int flip,
-    uint64_t *__restrict__ pl, int *changed, int opt, int *__restrict__ status)
+    int V, int VS, int W, const int32_t *__restrict__ ell_col, int ndst, int nbatch, int vpb,
+    int lvl, int flip, uint64_t *__restrict__ pl, int *changed, int opt, int *__restrict__ status)
 {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int batch = blockIdx.y;
+    // a block covers vpb vertices of blockDim / vpb batches: with vpb = 64
+    // its waves read the same 64 rows (one wave per batch), so the row
+    // loads after the first hit the CU's L1
+    const int x = blockIdx.x * vpb + (int)threadIdx.x % vpb;
+    const int batch = blockIdx.y * ((int)blockDim.x / vpb) + (int)threadIdx.x / vpb;
+    if (batch >= nbatch) return;
     // levels are queued ahead of the host's termination check: a level
     // after one that reached nothing has nothing to do
     if (lvl > 1 && __hip_atomic_load(&changed[lvl - 1], __ATOMIC_RELAXED,
@@ -1016,6 +1020,13 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
     bool small = (size_t)gx * nbatch < 2 * (size_t)ctx->num_cus;
     if (const char *f = getenv("SDNROUTE_PLANE_BLOCK")) small = atoi(f) == 64;
     const int lb = small ? 64 : 256;
+    // level pass: batches per block on small graphs (SDNROUTE_PLANE_BPB=2|4;
+    // 4 measured k=48 0.0917 -> 0.0926 ms, dragonfly 0.0625 -> 0.0608 ms)
+    int bpb = 1;
+    if (const char *f = getenv("SDNROUTE_PLANE_BPB")) {
+        const int k = atoi(f);
+        if (small && (k == 1 || k == 2 || k == 4)) bpb = k;
+    }
     for (int c0 = 0; c0 < nbatch; c0 += cb) {
         const int nbc = nbatch - c0 < cb ? nbatch - c0 : cb;
         const int nd = ndst - c0 * 64 < nbc * 64 ? ndst - c0 * 64 : nbc * 64;
@@ -1047,9 +1058,9 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
             if (upto > 255) upto = 255;
             for (; lvl <= upto; ++lvl) {
 #define SDNR_LEVEL(SB_)                                                                       \
-    hipLaunchKernelGGL(msbfs_plane_level_kernel<SB_>, dim3((V + lb - 1) / lb, nbc), dim3(lb), 0,  \
-                       ctx->stream, V, VS, W, ctx->ell_col, nd, lvl, (lvl - 1) & 1, pl, changed,  \
-                       popt, status)
+    hipLaunchKernelGGL(msbfs_plane_level_kernel<SB_>, dim3((V + lb - 1) / lb, (nbc + bpb - 1) / bpb), \
+                       dim3(lb * bpb), 0, ctx->stream, V, VS, W, ctx->ell_col, nd, nbc, lb, lvl,  \
+                       (lvl - 1) & 1, pl, changed, popt, status)
                 if (sb == 3) SDNR_LEVEL(3);
                 else if (sb == 4) SDNR_LEVEL(4);
                 else if (sb == 5) SDNR_LEVEL(5);
