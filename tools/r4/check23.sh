@@ -2,7 +2,7 @@
 # round 4: the next candidate chosen in the row step (its row prefetched, one
 # ballot -> readlane chain per candidate) vs the previous commit's search
 # (tools/r4/ab/libsdnroute_prev.so)
-OUT=gpurun_out/r4_c23; mkdir -p $OUT
+OUT=gpurun_out/${CHK_OUT:-r4_c23}; mkdir -p $OUT
 PREV=$PWD/tools/r4/ab/libsdnroute_prev.so
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
   tests/test_gpu_parity.py tests/test_fullsize_parity.py tests/test_events.py tests/test_topologydb_dropin.py -m gpu -k "dfs or async or tree or event or slot or route or pool" > $OUT/pytest.log 2>&1
