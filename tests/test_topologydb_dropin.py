@@ -687,3 +687,25 @@ def test_switch_fdb_entries_gpu():
     for fabric in (T.fat_tree(8), T.fat_tree(48)):
         db = fabric.populate(TopologyDB())
         _switch_fdb_check(db, fabric, np.random.default_rng(4))
+
+
+@pytest.mark.gpu
+def test_route_entries_wide_host_port(monkeypatch):
+    """A destination host port above 0xffff cannot ride in the u32 entry
+    (switch | port << 16): route_entries must take the int32 expansion and
+    still equal the reference's fdbs; the u32 form serves the other pairs."""
+    from oracle import oracle as O
+    from sdnmpi_amd import topologies as T
+    fabric = T.fat_tree(4)
+    db = fabric.populate(TopologyDB())
+    macs = sorted(db.hosts)
+    wide = macs[3]
+    h = db.hosts[wide]
+    db.add_host(Host(wide, Port(h.port.dpid, 70000)))
+    pairs = [(a, b) for a in macs for b in macs]
+    want = [O.find_route_pair(db, a, b) for a, b in pairs]
+    assert db.find_routes(pairs) == want
+    assert db.engine.ctx.last_kernel() == "route_seg_packed_kernel<1024>"   # int32 form
+    narrow = [(a, b) for a, b in pairs if b != wide]
+    assert db.find_routes(narrow) == [O.find_route_pair(db, a, b) for a, b in narrow]
+    assert db.engine.ctx.last_kernel() == "route_seg_packed_kernel<1024,u32>"
