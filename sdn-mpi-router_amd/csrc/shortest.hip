@@ -835,7 +835,7 @@ __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
 // wave hit 32 different banks, instead of two scattered global loads per
 // (destination, vertex)
 template <int SB, int TB, int Q>
-__global__ __launch_bounds__(256) void msbfs_plane_tables_kernel(
+__global__ __launch_bounds__(TB * Q) void msbfs_plane_tables_kernel(
     int V, int VS, int W, const int32_t *__restrict__ ell_col, const int32_t *__restrict__ ell_port,
     int ndst, const uint64_t *__restrict__ pl, uint16_t *__restrict__ dist,
     int32_t *__restrict__ nh, int32_t *__restrict__ nh_port, const int *__restrict__ status,
