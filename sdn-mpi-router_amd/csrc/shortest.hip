@@ -672,6 +672,11 @@ constexpr int kPlVis = 0, kPlFront = 1, kPlNext = 2, kPlDist = 3, kPlSlot = 11;
 // planes per batch: vis, front, next, 8 level, SB slot planes (SB =
 // ceil(log2 W)); 16 (a 4 MiB batch stride on the torus) up to SB = 5
 __host__ __device__ constexpr int plane_count(int sb) { return sb <= 5 ? 16 : kPlSlot + sb; }
+// DP: level planes.  8 (levels < 256), or 3 when the BFS is known to end by
+// level 7 (the previous call's depth): planes [vis, front, next, 3 level,
+// sb slot] -- k=48 12 planes instead of 17, so the init writes, the table
+// pass reads and the chunks' footprint shrink with them
+__host__ __device__ constexpr int plane_count_dp(int sb, int dp) { return dp == 8 ? plane_count(sb) : 3 + dp + sb; }
 
 __global__ __launch_bounds__(256) void msbfs_plane_seed_kernel(
     int V, int VS, const int32_t *__restrict__ dst, int ndst, uint64_t *__restrict__ pl, int npl,
@@ -745,7 +750,7 @@ constexpr int kPlAtomicOr = 2;
 // (a per-wave store and atomic on two single hot words cost the 32^3 torus
 // 12 -> 33 ms; a per-workgroup update behind a barrier 14.7 ms)
 constexpr int kStatusWords = 256;
-template <int SB>
+template <int SB, int DP>
 __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
     int V, int VS, int W, const int32_t *__restrict__ ell_col, int ndst, int nbatch, int vpb,
     int lvl, int flip, uint64_t *__restrict__ pl, int *changed, int opt, int *__restrict__ status)
@@ -761,7 +766,7 @@ __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
     if (lvl > 1 && __hip_atomic_load(&changed[lvl - 1], __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT) == 0) return;
     if (x >= V) return;
-    uint64_t *b = pl + (size_t)batch * plane_count(SB) * VS;
+    uint64_t *b = pl + (size_t)batch * plane_count_dp(SB, DP) * VS;
     const uint64_t *front = b + (size_t)(flip ? kPlNext : kPlFront) * VS;
     uint64_t *next = b + (size_t)(flip ? kPlFront : kPlNext) * VS;
     const int nb = min(64, ndst - batch * 64);
@@ -812,19 +817,19 @@ __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
         b[(size_t)kPlVis * VS + x] = vx | nw;
         if (opt & kPlAtomicOr) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
+            for (int k = 0; k < DP; ++k)
                 if ((lvl >> k) & 1)
                     atomicOr((unsigned long long *)&b[(size_t)(kPlDist + k) * VS + x], nw);
 #pragma unroll
             for (int k = 0; k < SB; ++k)
-                if (sp[k]) atomicOr((unsigned long long *)&b[(size_t)(kPlSlot + k) * VS + x], sp[k]);
+                if (sp[k]) atomicOr((unsigned long long *)&b[(size_t)(kPlDist + DP + k) * VS + x], sp[k]);
         } else {
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
+            for (int k = 0; k < DP; ++k)
                 if ((lvl >> k) & 1) b[(size_t)(kPlDist + k) * VS + x] |= nw;
 #pragma unroll
             for (int k = 0; k < SB; ++k)
-                if (sp[k]) b[(size_t)(kPlSlot + k) * VS + x] |= sp[k];
+                if (sp[k]) b[(size_t)(kPlDist + DP + k) * VS + x] |= sp[k];
         }
     }
 }
@@ -834,7 +839,7 @@ __global__ __launch_bounds__(256) void msbfs_plane_level_kernel(
 // once, transposed to [slot][vertex] so the per-destination lookups of a
 // wave hit 32 different banks, instead of two scattered global loads per
 // (destination, vertex)
-template <int SB, int TB, int Q>
+template <int SB, int TB, int Q, int DP>
 __global__ __launch_bounds__(TB * Q) void msbfs_plane_tables_kernel(
     int V, int VS, int W, const int32_t *__restrict__ ell_col, const int32_t *__restrict__ ell_port,
     int ndst, const uint64_t *__restrict__ pl, uint16_t *__restrict__ dist,
@@ -885,13 +890,13 @@ __global__ __launch_bounds__(TB * Q) void msbfs_plane_tables_kernel(
         __syncthreads();
     }
     if (x >= V) return;
-    const uint64_t *b = pl + (size_t)batch * plane_count(SB) * VS;
+    const uint64_t *b = pl + (size_t)batch * plane_count_dp(SB, DP) * VS;
     const uint64_t vx = b[(size_t)kPlVis * VS + x];
-    uint64_t d[8], s[SB];
+    uint64_t d[DP], s[SB];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) d[k] = b[(size_t)(kPlDist + k) * VS + x];
+    for (int k = 0; k < DP; ++k) d[k] = b[(size_t)(kPlDist + k) * VS + x];
 #pragma unroll
-    for (int k = 0; k < SB; ++k) s[k] = b[(size_t)(kPlSlot + k) * VS + x];
+    for (int k = 0; k < SB; ++k) s[k] = b[(size_t)(kPlDist + DP + k) * VS + x];
     const int nb = min(64, ndst - batch * 64);
     // 8 destinations at a time: the planes shifted once per group (32-bit
     // bit extracts after that), the group's 16 LDS lookups issued together
@@ -900,9 +905,9 @@ __global__ __launch_bounds__(TB * Q) void msbfs_plane_tables_kernel(
     const int iend = min(nb, (q + 1) * (64 / Q));
     for (int i0 = q * (64 / Q); i0 < iend; i0 += CG) {
         const uint32_t vv = (uint32_t)(vx >> i0);
-        uint32_t dv[8], sv[SB];
+        uint32_t dv[DP], sv[SB];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) dv[k] = (uint32_t)(d[k] >> i0);
+        for (int k = 0; k < DP; ++k) dv[k] = (uint32_t)(d[k] >> i0);
 #pragma unroll
         for (int k = 0; k < SB; ++k) sv[k] = (uint32_t)(s[k] >> i0);
         uint32_t L[CG];
@@ -915,7 +920,7 @@ __global__ __launch_bounds__(TB * Q) void msbfs_plane_tables_kernel(
             if ((vv >> u) & 1u) {
                 uint32_t l = 0;
 #pragma unroll
-                for (int k = 0; k < 8; ++k) l |= ((dv[k] >> u) & 1u) << k;
+                for (int k = 0; k < DP; ++k) l |= ((dv[k] >> u) & 1u) << k;
                 L[u] = l;
                 if (l && nh) {
                     int sl = 0;
@@ -950,9 +955,12 @@ static const char *sp_strategy()
 }
 
 // bit-plane BFS (msbfs_plane_*): returns 1 (nothing launched that matters,
-// tables to be redone) if a BFS is deeper than the 255 levels the planes hold
-static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint16_t *d_dist,
-                        int32_t *d_nh, int32_t *d_nh_port)
+// tables to be redone) if a BFS is deeper than the 255 levels the planes hold;
+// with compact planes (3 level planes), kPlaneDeeper once a BFS runs past
+// level 7 (the caller redoes the call with 8)
+constexpr int kPlaneDeeper = 3;
+static int launch_plane_dp(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint16_t *d_dist,
+                           int32_t *d_nh, int32_t *d_nh_port, bool compact)
 {
     const int V = ctx->V, W = ctx->W;
     const int sb = W <= 8 ? 3 : W <= 16 ? 4 : W <= 32 ? 5 : 6;
@@ -968,7 +976,8 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
         const int pad = atoi(f);                              // overlap the planes
         if (pad >= 0 && pad <= (1 << 16)) VS = V + pad;
     }
-    const size_t per_batch = (size_t)plane_count(sb) * VS * sizeof(uint64_t);
+    const int npl = plane_count_dp(sb, compact ? 3 : 8);
+    const size_t per_batch = (size_t)npl * VS * sizeof(uint64_t);
     // batches per chunk: the planes one level sweeps stay inside the 256 MiB
     // Infinity Cache (measured: torus 32^3 14.9 -> 12.8 ms with 64 batches of
     // 4 MiB instead of all 512 at once; the 100k Jellyfish 127 -> 119 ms)
@@ -1011,9 +1020,14 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
     const char *iq = getenv("SDNROUTE_PLANE_INIT");
     const bool oldinit = iq && !strcmp(iq, "0");
     const size_t tl = d_nh ? (size_t)2 * W * 257 * sizeof(int32_t) : 0;   // kTabStride, TB 256
-    if (sb == 5 && tl > 65536)   // W = 32 with the padded stride
-        sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<5, 256, 1>), tl);
-    if (sb == 6) sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<6, 256, 1>), tl);
+    if (sb == 5 && tl > 65536) {  // W = 32 with the padded stride
+        sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<5, 256, 1, 8>), tl);
+        sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<5, 256, 1, 3>), tl);
+    }
+    if (sb == 6) {
+        sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<6, 256, 1, 8>), tl);
+        sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<6, 256, 1, 3>), tl);
+    }
     // small launches (fewer 256-vertex blocks than 2 per CU over the whole
     // destination set): 64-vertex blocks, so every CU gets work
     // (SDNROUTE_PLANE_BLOCK=256|64 overrides)
@@ -1038,11 +1052,11 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
                                     ctx->stream));
             if (!full) SDNR_HIP(hipMemsetAsync(changed, 0, kFlagInts * sizeof(int), ctx->stream));
             hipLaunchKernelGGL(msbfs_plane_seed_kernel, dim3((nd + 255) / 256), dim3(256), 0,
-                               ctx->stream, V, VS, d_dst + (size_t)c0 * 64, nd, pl, plane_count(sb),
+                               ctx->stream, V, VS, d_dst + (size_t)c0 * 64, nd, pl, npl,
                                status);
         } else {
             hipLaunchKernelGGL(msbfs_plane_init_kernel, dim3((VS + lb - 1) / lb, nbc), dim3(lb), 0,
-                               ctx->stream, V, VS, d_dst + (size_t)c0 * 64, nd, pl, plane_count(sb),
+                               ctx->stream, V, VS, d_dst + (size_t)c0 * 64, nd, pl, npl,
                                changed, kFlagInts, status);
         }
         SDNR_HIP(hipGetLastError());
@@ -1056,15 +1070,24 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
         for (;;) {
             upto = lvl <= guess ? guess : lvl + kGroup - 1;
             if (upto > 255) upto = 255;
+            if (compact && upto > 7) upto = 7;
             for (; lvl <= upto; ++lvl) {
-#define SDNR_LEVEL(SB_)                                                                       \
-    hipLaunchKernelGGL(msbfs_plane_level_kernel<SB_>, dim3((V + lb - 1) / lb, (nbc + bpb - 1) / bpb), \
-                       dim3(lb * bpb), 0, ctx->stream, V, VS, W, ctx->ell_col, nd, nbc, lb, lvl,  \
-                       (lvl - 1) & 1, pl, changed, popt, status)
-                if (sb == 3) SDNR_LEVEL(3);
-                else if (sb == 4) SDNR_LEVEL(4);
-                else if (sb == 5) SDNR_LEVEL(5);
-                else SDNR_LEVEL(6);
+#define SDNR_LEVEL(SB_, DP_)                                                                  \
+    hipLaunchKernelGGL((msbfs_plane_level_kernel<SB_, DP_>),                                      \
+                       dim3((V + lb - 1) / lb, (nbc + bpb - 1) / bpb), dim3(lb * bpb), 0,         \
+                       ctx->stream, V, VS, W, ctx->ell_col, nd, nbc, lb, lvl, (lvl - 1) & 1, pl,  \
+                       changed, popt, status)
+                if (compact) {
+                    if (sb == 3) SDNR_LEVEL(3, 3);
+                    else if (sb == 4) SDNR_LEVEL(4, 3);
+                    else if (sb == 5) SDNR_LEVEL(5, 3);
+                    else SDNR_LEVEL(6, 3);
+                } else {
+                    if (sb == 3) SDNR_LEVEL(3, 8);
+                    else if (sb == 4) SDNR_LEVEL(4, 8);
+                    else if (sb == 5) SDNR_LEVEL(5, 8);
+                    else SDNR_LEVEL(6, 8);
+                }
 #undef SDNR_LEVEL
                 SDNR_HIP(hipGetLastError());
             }
@@ -1073,25 +1096,28 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
             // the table pass runs (the next call's launches overlap it)
             const int seq = ++ctx->pub_seq;
             int *hp = ctx->h_pub;
-#define SDNR_TABLES(SB_, TB_, Q_)                                                               \
-    hipLaunchKernelGGL((msbfs_plane_tables_kernel<SB_, TB_, Q_>), dim3((V + TB_ - 1) / TB_, nbc), \
-                       dim3(TB_ * Q_), (size_t)(nh ? 2 * W * (TB_ + 1) * 4 : 0), ctx->stream, V, VS, \
-                       W, ctx->ell_col, ctx->ell_port, nd, pl, dist, nh, nhp, status, hp, seq)
-            if (small) {
-                if (sb == 3) SDNR_TABLES(3, 64, 4);
-                else if (sb == 4) SDNR_TABLES(4, 64, 4);
-                else if (sb == 5) SDNR_TABLES(5, 64, 4);
-                else SDNR_TABLES(6, 64, 4);
-            } else {
-                if (sb == 3) SDNR_TABLES(3, 256, 1);
-                else if (sb == 4) SDNR_TABLES(4, 256, 1);
-                else if (sb == 5) SDNR_TABLES(5, 256, 1);
-                else SDNR_TABLES(6, 256, 1);
-            }
+#define SDNR_TABLES(SB_, TB_, Q_, DP_)                                                          \
+    hipLaunchKernelGGL((msbfs_plane_tables_kernel<SB_, TB_, Q_, DP_>),                            \
+                       dim3((V + TB_ - 1) / TB_, nbc), dim3(TB_ * Q_),                             \
+                       (size_t)(nh ? 2 * W * (TB_ + 1) * 4 : 0), ctx->stream, V, VS, W,            \
+                       ctx->ell_col, ctx->ell_port, nd, pl, dist, nh, nhp, status, hp, seq)
+#define SDNR_TABLES_SB(TB_, Q_, DP_)                                                            \
+    do {                                                                                        \
+        if (sb == 3) SDNR_TABLES(3, TB_, Q_, DP_);                                              \
+        else if (sb == 4) SDNR_TABLES(4, TB_, Q_, DP_);                                         \
+        else if (sb == 5) SDNR_TABLES(5, TB_, Q_, DP_);                                         \
+        else SDNR_TABLES(6, TB_, Q_, DP_);                                                      \
+    } while (0)
+            if (small && compact) SDNR_TABLES_SB(64, 4, 3);
+            else if (small) SDNR_TABLES_SB(64, 4, 8);
+            else if (compact) SDNR_TABLES_SB(256, 1, 3);
+            else SDNR_TABLES_SB(256, 1, 8);
+#undef SDNR_TABLES_SB
 #undef SDNR_TABLES
             SDNR_HIP(hipGetLastError());
             if ((rc = sdnr_wait_published(ctx, seq, 2, st))) return rc;
             if ((long long)st[0] == target || st[1] < upto) break;
+            if (compact && upto >= 7) return kPlaneDeeper;   // past the 3 level planes
             if (upto == 255) return 1;           // deeper than 255 levels
         }
         levels += upto;
@@ -1107,6 +1133,24 @@ static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint1
     ctx->last_kernel = "msbfs_plane_level_kernel+msbfs_plane_tables_kernel";
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
     return SDNR_OK;
+}
+
+static int launch_plane(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint16_t *d_dist,
+                        int32_t *d_nh, int32_t *d_nh_port)
+{
+    // compact level planes when the previous call on this graph ended by
+    // level 7 (SDNROUTE_PLANE_DP=8 keeps the 8 planes); a deeper BFS redoes
+    // the call with 8
+    const char *f = getenv("SDNROUTE_PLANE_DP");
+    const char *gq = getenv("SDNROUTE_PLANE_GUESS");
+    const bool compact = !(f && !strcmp(f, "8")) && !(gq && !strcmp(gq, "0")) &&
+                         ctx->plane_depth >= 1 && ctx->plane_depth <= 7;
+    int rc = launch_plane_dp(ctx, d_dst, ndst, d_dist, d_nh, d_nh_port, compact);
+    if (rc == kPlaneDeeper) {
+        ctx->plane_depth = 0;
+        rc = launch_plane_dp(ctx, d_dst, ndst, d_dist, d_nh, d_nh_port, false);
+    }
+    return rc;
 }
 
 int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,

@@ -597,6 +597,28 @@ def test_shortest_plane_stride_pad(ctx, monkeypatch, name, pad):
     np.testing.assert_array_equal(nhp, nhpo)
 
 
+@pytest.mark.parametrize("dp", ["auto", "8"])
+def test_shortest_plane_compact_levels(ctx, monkeypatch, dp):
+    """Compact level planes (3 instead of 8) when the previous call on the
+    graph ended by level 7, and the redo with 8 when a call then runs
+    deeper: random_V40, whose destinations' eccentricities run 4..13 (some
+    pairs unreachable), with shallow and deep destination sets in turn on one
+    context, against the oracle (SDNROUTE_PLANE_DP=8: always 8 planes)."""
+    monkeypatch.setenv("SDNROUTE_SP_STRATEGY", "plane")
+    if dp != "auto":
+        monkeypatch.setenv("SDNROUTE_PLANE_DP", dp)
+    csr = G.Golden("random_V40").fabric().csr()
+    ctx.upload(csr)
+    for dsts in ([1, 6, 11, 12], [14, 7], [1, 6, 11, 12], [1, 6, 11, 12], [3, 25, 5],
+                 [13, 39], list(range(csr.V))):
+        dsts = np.asarray(dsts, np.int32)
+        dist, nh, nhp = ctx.shortest_tables(dsts)
+        do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
+        np.testing.assert_array_equal(dist, do)
+        np.testing.assert_array_equal(nh, nho)
+        np.testing.assert_array_equal(nhp, nhpo)
+
+
 @pytest.mark.parametrize("strategy", ["auto", "msbfs", "plane", "lanes"])
 def test_shortest_fullsize_torus_sample(ctx, monkeypatch, strategy):
     """torus 32^3 (the BASELINE multi-source BFS config), spread destinations:
