@@ -117,11 +117,15 @@ def record_traffic(pmc, key, kernel_prefix, path, steps=None):
         hits = [d for k, d in pmc.items() if pre in k]
         if not hits:
             raise SystemExit("no PMC rows for kernel %r" % pre)
-        c = hits[0]["counters"]
-        if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
-            raise SystemExit("FETCH_SIZE / WRITE_SIZE missing for %r" % pre)
-        per = hbm_bytes(c)
-        tb += per * (hits[0]["dispatches"] / float(steps) if len(prefixes) > 1 else 1.0)
+        if len(prefixes) == 1:
+            hits = hits[:1]
+        # a step of several kernels: every instantiation matching the prefix
+        # (e.g. the plane BFS's 8- and 3-level-plane variants) counts
+        for h in hits:
+            c = h["counters"]
+            if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
+                raise SystemExit("FETCH_SIZE / WRITE_SIZE missing for %r" % pre)
+            tb += hbm_bytes(c) * (h["dispatches"] / float(steps) if len(prefixes) > 1 else 1.0)
     data = json.load(open(path)) if os.path.exists(path) else {}
     data[key] = tb
     json.dump(data, open(path, "w"), indent=1, sort_keys=True)
