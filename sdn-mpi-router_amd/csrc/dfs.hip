@@ -1528,7 +1528,17 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
 #ifndef SDNR_ASYNC_G
 #define SDNR_ASYNC_G 16
 #endif
-    constexpr int G = NW <= 4 ? SDNR_ASYNC_G : 8;   // rows in flight per worker
+#ifndef SDNR_ASYNC_G_DW
+#define SDNR_ASYNC_G_DW 16
+#endif
+#ifndef SDNR_ASYNC_G_P1
+#define SDNR_ASYNC_G_P1 8
+#endif
+    // children per worker step: 16 (8 above 4 waves), and 16 with the
+    // dword-paired rows of the 5-worker regime (8 loads): k=48 144 sources
+    // 54.9 -> 48.8 us, one source 53.3 -> 47.2 us (fresher counts)
+    constexpr int G = NW <= 4 ? SDNR_ASYNC_G
+                              : (PAIR == 2 ? SDNR_ASYNC_G_DW : (PAIR == 1 ? SDNR_ASYNC_G_P1 : 8));
     constexpr unsigned kSpin = 1u << 22;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int VW = (V + 1 + 31) >> 5;
