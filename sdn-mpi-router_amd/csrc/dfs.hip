@@ -2213,8 +2213,10 @@ static int dfs_async_waves(const sdnr_ctx *ctx, int nsrc)
     // sources 63.4 / 64.3 / 65.1 / 69.1 -> 56.8 / 58.4 / 59.4 / 64.2 us,
     // dragonfly 258 sources 127.7 -> 120.8 us; equal at 576 sources, and
     // slower once every CU holds several sources (k=48 1,152: 91.6 -> 137 us
-    // with 4 workers), where the workers compete with the search waves
-    if (nsrc <= 2 * ctx->num_cus) return 6;
+    // with 4 workers), where the workers compete with the search waves.
+    // Round 4: with the dword-paired rows (in-degree > 32) 7 workers -- k=48
+    // 144 / 1 sources 48.8 / 47.1 -> 46.9 / 45.1 us
+    if (nsrc <= 2 * ctx->num_cus) return ctx->radj_pair ? 6 : 8;
     return ctx->max_deg <= 32 ? 3 : 4;
 }
 
@@ -2558,7 +2560,7 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         // u16 rows stay there (SDNROUTE_DFS_DW=0|1 forces either)
         const bool pair = preswz && ctx->radj_pair;
         const char *dq = getenv("SDNROUTE_DFS_DW");
-        bool dw = preswz && !pair && !c16 && nw == 6;
+        bool dw = preswz && !pair && !c16 && nw >= 6;
         if (dq) dw = preswz && !pair && !c16 && !strcmp(dq, "1");
         int cgrid = (int)((size_t)ctx->num_cus * cpc);
         if (cgrid > nsrc) cgrid = nsrc;
