@@ -78,6 +78,10 @@ def parse():
                     help="N > 1: tables assembled on every rank (RCCL all-gather, default) "
                          "or on rank 0 only (point-to-point receives into the root); the "
                          "other form is measured beside it in the multi_gpu block")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="launcher rehearsal on CPU: the N ranks form a gloo group, shard "
+                         "the sources and assemble them, and rank 0 prints the line's "
+                         "multi-rank keys -- no GPU call, no kernel (tests only)")
     return ap.parse_args()
 
 
@@ -731,15 +735,98 @@ def multi_gpu_extras(args, world, rank, local, dev, csr, srcs, per, packed, slot
     return res
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """``--gpus N`` (N > 1) run without a launcher: start the N rank
+    processes under torch.distributed.run (one process per GPU, RCCL over
+    xGMI; rendezvous on 127.0.0.1) and return their exit status.  This
+    process makes no GPU call at all -- the ranks are children, nothing is
+    exec'd -- and each rank checks that the process group it forms has
+    exactly N members on N distinct devices."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")     # dmabuf IPC only on this driver
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def rank_devices(dev, local):
+    """Every rank's (rank, local device index, device uuid) in rank order --
+    the multi-GPU line names the devices it ran on."""
+    props = torch.cuda.get_device_properties(dev)
+    mine = (dist.get_rank(), local, "pci %04x:%02x:%02x" % (
+        props.pci_domain_id, props.pci_bus_id, props.pci_device_id))
+    every = [None] * dist.get_world_size()
+    dist.all_gather_object(every, mine)
+    return every
+
+
+def main_rehearse(args, world, rank):
+    """The N-rank launch path without a GPU (CPU tests): the ranks form a
+    gloo group, take their contiguous source shards exactly as the bench
+    does, assemble them with the bench's all-gather helper, and rank 0
+    prints the multi-rank keys of the line.  No kernel runs: the timing is
+    the assembly of the source ids only."""
+    dist.init_process_group("gloo")
+    fabric = T.by_name(args.fabric)
+    hv, _ = fabric.host_table()
+    srcs = np.unique(hv).astype(np.int32)
+    lo, hi, per = D.shard_bounds(len(srcs), world, rank)
+    mine = D.padded_shard(srcs, world, rank).view(per, 1)
+    out = torch.empty((world * per, 1), dtype=torch.int32)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(max(1, args.steps)):
+        D.all_gather_rows_async(mine, out).wait()
+    dist.barrier()
+    elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    shards = [None] * world
+    dist.all_gather_object(shards, (rank, lo, hi, os.getpid()))
+    ok = bool(np.array_equal(D.unpad(out.view(-1), len(srcs)).numpy(), srcs))
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "rehearsal": True, "value": None, "n_gpus": world,
+            "steps": args.steps, "ms_per_step": float(elapsed.item()) / max(1, args.steps) * 1e3,
+            "process_group": {"backend": dist.get_backend(), "world_size": dist.get_world_size()},
+            "config": {"fabric": args.fabric, "sources": len(srcs),
+                       "parallelism": "sources sharded over %d rank(s)" % world},
+            "shards": [{"rank": r, "lo": a, "hi": b, "pid": p} for r, a, b, p in shards],
+            "sources_assembled_exactly": ok}), flush=True)
+    dist.destroy_process_group()
+    return 0 if ok else 1
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher around us: become the launcher (before any GPU call)
+        sys.exit(launch_ranks(args))
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: %d ranks were launched (WORLD_SIZE) but --gpus is %d"
+                         % (world, args.gpus))
+    if args.rehearse:
+        sys.exit(main_rehearse(args, world, rank) if world > 1 else 0)
     # BENCH_DEVICE pins every rank to one device (rehearsing the N > 1 code
     # path on a one-GPU box); the driver never sets it
     if os.environ.get("BENCH_DEVICE"):
         local = int(os.environ["BENCH_DEVICE"])
+    elif torch.cuda.device_count() < world:      # counts devices without initialising HIP
+        raise SystemExit("bench.py: --gpus %d but only %d GPU(s) are visible"
+                         % (world, torch.cuda.device_count()))
     ref_mp = None
     if world == 1 and args.mode == "dfs" and not args.no_cpu_baseline:
         # forks: must run before the first GPU call of this process
@@ -753,6 +840,13 @@ def main():
             dist.init_process_group(backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    devices = None
+    if world > 1:
+        devices = rank_devices(dev, local)
+        uuids = {d[2] for d in devices}
+        if len(uuids) != world and not os.environ.get("BENCH_DEVICE"):
+            raise SystemExit("bench.py: %d ranks share %d device(s): %r"
+                             % (world, len(uuids), devices))
     if args.mode == "flows":
         return main_flows(args, world, rank, local, dev)
     if args.mode == "ecmp":
@@ -929,6 +1023,11 @@ def main():
         "teps": float(hi - lo) * E / (kern_ms / 1e3),
     }
     if multi is not None:
+        multi["process_group"] = {"backend": dist.get_backend(),
+                                  "world_size": dist.get_world_size()}
+        if dist.get_backend() == "nccl":
+            multi["rccl_world_size"] = dist.get_world_size()
+        multi["devices"] = [{"rank": r, "local": l, "device": d} for r, l, d in devices]
         out["multi_gpu"] = multi
         out["config"]["assemble"] = args.assemble
     if rank == 0 and world == 1 and args.mode == "dfs" and \

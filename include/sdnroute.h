@@ -53,6 +53,12 @@ typedef struct sdnr_ctx sdnr_ctx;
 /* ABI version of the loaded library (== SDNR_ABI_VERSION it was built with) */
 int sdnr_abi_version(void);
 
+/* Build identity: the SHA-256 (64 hex digits) of the sources, headers and
+ * compile flags the library was built from ("unversioned" for a build made
+ * without it).  The Python loader refuses a library whose id is not the
+ * tree's (sdn-mpi-router_amd/sdnmpi_amd/_buildinfo.py). */
+const char *sdnr_build_id(void);
+
 /* Message of the last failing call on this thread ("" if none). */
 const char *sdnr_last_error(void);
 

@@ -138,6 +138,7 @@ static void free_graph(sdnr_ctx *c)
 
 static constexpr size_t kPad = SDNR_WAVE;
 
+#ifdef SDNR_DIAG_VARIANTS
 // Sorted rows (stride-64 u16 rows padded with the sentinel V) as arithmetic
 // runs for dfs_runs.hip: greedy longest progression from each position,
 // strides <= 511, counts <= 64, a run word = start | stride << 16 | count <<
@@ -170,6 +171,8 @@ static int encode_runs(int32_t V, const std::vector<uint16_t> &rows, int R,
     return most;
 }
 
+#endif
+
 // device copy of `bytes` plus `pad` int32 entries of -1 behind them
 static int upload(int32_t **dst, const void *src, size_t bytes, size_t pad, hipStream_t s)
 {
@@ -181,12 +184,22 @@ static int upload(int32_t **dst, const void *src, size_t bytes, size_t pad, hipS
     return SDNR_OK;
 }
 
+// build identity: SHA-256 of the sources, headers and flags this library was
+// compiled from (sdnmpi_amd/_buildinfo.py passes it; a file scan finds the
+// marker without loading the library)
+#ifndef SDNR_BUILD_ID
+#define SDNR_BUILD_ID "unversioned"
+#endif
+static const char k_build_marker[] __attribute__((used)) = "SDNR_BUILD_ID:" SDNR_BUILD_ID;
+
 #define CHECK_CTX(c) \
     if (!(c)) return sdnr_fail(SDNR_ERR_INVAL, "%s: null context", __func__)
 
 extern "C" {
 
 int sdnr_abi_version(void) { return SDNR_ABI_VERSION; }
+
+const char *sdnr_build_id(void) { return k_build_marker + sizeof("SDNR_BUILD_ID:") - 1; }
 
 const char *sdnr_last_error(void) { return g_err; }
 
@@ -538,6 +551,8 @@ static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *
                 if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
             }
         }
+#ifdef SDNR_DIAG_VARIANTS
+        // diagnostic build only (tools/diag/): the losing DFS variants' rows
         // the out-rows as arithmetic runs for the LDS-row DFS (dfs_runs.hip)
         const char *rf = getenv("SDNROUTE_RUNS");                 // 0: off (A/B)
         if (he == hipSuccess && maxin <= SDNR_WAVE && !(rf && !strcmp(rf, "0"))) {
@@ -594,6 +609,7 @@ static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *
                                     ctx->stream);
             if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
         }
+#endif
         if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
         if (he != hipSuccess) {
             free_graph(ctx);

@@ -148,6 +148,8 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
 // int32 trees -> parent | port << 16 or parent | slot << 26 (dfs.hip)
 int sdnr_launch_tree_pack(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port, size_t n,
                           uint32_t *tree, bool slots);
+#ifdef SDNR_DIAG_VARIANTS
+// the diagnostic build's losing DFS variants (tools/diag/)
 // register-visited DFS (dfs_bits.hip): V <= 4096 with bitmap rows uploaded
 bool sdnr_dfs_bits_ok(const sdnr_ctx *ctx);
 int sdnr_launch_dfs_bits(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, int32_t *d_parent,
@@ -157,6 +159,7 @@ int sdnr_launch_dfs_bits(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, int3
 bool sdnr_dfs_runs_ok(const sdnr_ctx *ctx, bool hops);
 int sdnr_launch_dfs_runs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, int32_t *d_parent,
                          int32_t *d_port, int32_t *d_hops, uint32_t *d_tree);
+#endif
 int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
                          uint16_t *d_dist, int32_t *d_nh, int32_t *d_nh_port);
 int sdnr_launch_apsp(sdnr_ctx *ctx, uint16_t *d_dist);

@@ -2408,12 +2408,15 @@ int sdnr_launch_tree_pack(sdnr_ctx *ctx, const int32_t *parent, const int32_t *p
     return SDNR_OK;
 }
 
+#ifdef SDNR_DIAG_VARIANTS
 // the register-visited kernel (dfs_bits.hip) where it applies: forced with
 // SDNROUTE_DFS_STRATEGY=bits (A/B; not yet the default)
 static bool dfs_bits_default(const char *force)
 {
     return force && !strcmp(force, "bits");
 }
+
+#endif
 
 // hop counts as u16 (0xFFFF unreached) into d_hops
 __global__ __launch_bounds__(256) void dfs_hops16_kernel(size_t n, const int32_t *__restrict__ h,
@@ -2467,6 +2470,9 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
               ctx->port};
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
     const char *force = getenv("SDNROUTE_DFS_STRATEGY");
+#ifdef SDNR_DIAG_VARIANTS
+    // diagnostic build only (tools/diag/build_diag.sh): the two losing
+    // variants of DESIGN.md 4.1a / 4.1b, forced by SDNROUTE_DFS_STRATEGY
     // rows in LDS as arithmetic runs (dfs_runs.hip), SDNROUTE_DFS_STRATEGY=
     // runs: measured no faster than dfs_async_kernel, so
     // opt-in
@@ -2484,6 +2490,7 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
         return SDNR_OK;
     }
+#endif
     const bool count_ok = ctx->adj16 != nullptr && ctx->radj16 != nullptr && V < 65535 &&
                           dfs_lds_bytes_count(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;
     const bool async_ok = count_ok && dfs_lds_bytes_async(V, hops) <= SDNR_MAX_LDS_PER_BLOCK;

@@ -33,7 +33,7 @@ ABI_VERSION = 1
 
 # every entry point declared in include/sdnroute.h
 EXPORTED_SYMBOLS = (
-    "sdnr_abi_version", "sdnr_last_error", "sdnr_device_count", "sdnr_create",
+    "sdnr_abi_version", "sdnr_build_id", "sdnr_last_error", "sdnr_device_count", "sdnr_create",
     "sdnr_create_multi", "sdnr_device_list", "sdnr_destroy", "sdnr_set_stream", "sdnr_synchronize", "sdnr_graph_upload",
     "sdnr_graph_info", "sdnr_dfs_tables", "sdnr_dfs_tables_packed", "sdnr_dfs_tables_slots",
     "sdnr_dfs_tables_tree", "sdnr_tree_pack", "sdnr_shortest_tables", "sdnr_route_expand_packed",
@@ -66,6 +66,7 @@ def _bind(L):
     c_int, i32, u32, vp = ctypes.c_int, ctypes.c_int32, ctypes.c_uint32, ctypes.c_void_p
     sig = {
         "sdnr_abi_version": ([], c_int),
+        "sdnr_build_id": ([], ctypes.c_char_p),
         "sdnr_last_error": ([], ctypes.c_char_p),
         "sdnr_device_count": ([ctypes.POINTER(c_int)], c_int),
         "sdnr_create": ([c_int, ctypes.POINTER(vp)], c_int),
@@ -131,8 +132,27 @@ def library():
         if L.sdnr_abi_version() != ABI_VERSION:
             raise NativeUnavailable("ABI mismatch: library %d, binding %d"
                                     % (L.sdnr_abi_version(), ABI_VERSION))
+        if "SDNROUTE_LIB" not in os.environ:     # A/B and diagnostic builds are named explicitly
+            verify_build(L)
         _lib = L
         return L
+
+
+def verify_build(L, csrc=None, include=None):
+    """Refuse a library that was not built from the tree beside it: its
+    sdnr_build_id() must equal the SHA-256 of the current sources, headers
+    and flags (_buildinfo.tree_build_id).  Skipped when the sources are not
+    there (a package installed without csrc/)."""
+    from . import _buildinfo as B
+    want = B.tree_build_id(csrc or B.CSRC, include or B.INCLUDE)
+    if want is None:
+        return
+    got = L.sdnr_build_id().decode("ascii", "replace")
+    if got != want:
+        raise NativeUnavailable(
+            "stale %s: built from sources %s, the tree is %s -- rebuild with "
+            "`python -c 'import __graft_entry__ as g; g.build()'`" % (library_path(), got[:16],
+                                                                    want[:16]))
 
 
 def _check(rc):

@@ -64,3 +64,34 @@ def test_built_for_gfx950_only():
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
     for other in (b"--gfx942", b"--gfx90a", b"--gfx1100", b"--gfx908"):
         assert other not in blob
+
+
+def test_library_build_id_is_the_trees():
+    """The loaded library was compiled from exactly these sources (the id is
+    checked by the loader; here it is read both ways)."""
+    from sdnmpi_amd import _buildinfo as B
+    L = _native.library()
+    want = B.tree_build_id()
+    assert want is not None and len(want) == 64
+    assert L.sdnr_build_id().decode() == want
+    assert B.file_build_id(_native.library_path()) == want
+
+
+def test_loader_refuses_stale_library(tmp_path):
+    """Edit one hashed input (a copy of the tree's sources) and the loader's
+    check refuses the library built from the unedited tree."""
+    import shutil
+    from sdnmpi_amd import _buildinfo as B
+    L = _native.library()
+    csrc, inc = tmp_path / "csrc", tmp_path / "include"
+    shutil.copytree(B.CSRC, csrc)
+    shutil.copytree(B.INCLUDE, inc)
+    _native.verify_build(L, str(csrc), str(inc))          # identical copy: accepted
+    for label, path in B.inputs(str(csrc), str(inc)):
+        if label.endswith("dfs.hip"):
+            with open(path, "a") as f:
+                f.write("\n// edited\n")
+    assert B.tree_build_id(str(csrc), str(inc)) != B.tree_build_id()
+    with pytest.raises(_native.NativeUnavailable) as ei:
+        _native.verify_build(L, str(csrc), str(inc))
+    assert "stale" in str(ei.value)
