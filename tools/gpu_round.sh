@@ -11,7 +11,7 @@ mkdir -p "$OUT"
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 in $2"; exit $1;; esac; }
 K=()
 [ -n "${2:-}" ] && K=(-k "$2")
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --durations=60 --timeout 300 --timeout-method thread \
   "${K[@]}" > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -4 "$OUT/pytest_gpu.log"; fatal $rc pytest
 [ $rc -ne 0 ] && exit $rc
