@@ -43,6 +43,9 @@ int sdnr_check_watchdog(sdnr_ctx *ctx)
     SDNR_HIP(hipMemcpy(&h, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (h) {
         SDNR_HIP(hipMemset(ctx->d_err, 0, sizeof(int)));
+        if (h == kErrLastPort)
+            return sdnr_fail(SDNR_ERR_INVAL, "sdnr_route_expand_packed: a last port outside "
+                             "[0, 0xFFFF] (u32 entries hold 16-bit ports): entries invalid");
         return sdnr_fail(SDNR_ERR_HIP, "kernel watchdog tripped (code %d): results invalid", h);
     }
     return SDNR_OK;

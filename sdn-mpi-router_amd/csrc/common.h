@@ -119,6 +119,11 @@ inline void sdnr_allow_lds(const void *fn, size_t bytes)
         (void)hipGetLastError();
 }
 
+// watchdog-word codes a kernel ORs into ctx->d_err (dfs.hip uses 1..16 for
+// bounded waits that ran out); sdnr_synchronize turns a nonzero word into an
+// error
+constexpr int kErrLastPort = 256;   // sdnr_route_expand_packed: a last port outside [0, 0xFFFF]
+
 // error plumbing (capi.hip)
 int sdnr_fail(int code, const char *fmt, ...);
 int sdnr_hip_fail(hipError_t e, const char *what);

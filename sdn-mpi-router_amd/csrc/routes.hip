@@ -273,7 +273,7 @@ __global__ __launch_bounds__(256) void route_seg_packed_kernel(
     int V, const uint32_t *__restrict__ tree, Anc16 anc,
     const int32_t *__restrict__ rows, const int32_t *__restrict__ dsts,
     const int32_t *__restrict__ last_port, int npairs, const int64_t *__restrict__ off,
-    int32_t *__restrict__ hop_switch, int32_t *__restrict__ hop_port)
+    int32_t *__restrict__ hop_switch, int32_t *__restrict__ hop_port, int *__restrict__ err)
 {
     __shared__ uint32_t seg_lds[4][CAP];
     __shared__ int lp_lds[4][64];
@@ -299,6 +299,12 @@ __global__ __launch_bounds__(256) void route_seg_packed_kernel(
                 lo = off[i];
                 L = (int)(off[i + 1] - lo);
             }
+            // u32 entries hold a 16-bit port: a last (host) port outside
+            // [0, 0xFFFF] cannot be written -- fail the call (watchdog code
+            // kErrLastPort, reported by sdnr_synchronize) instead of keeping
+            // its low bits
+            if (OUTP && __ballot(L > 0 && (uint32_t)lp > 0xFFFFu) && lane == 0)
+                atomicOr(err, kErrLastPort);
             const int pl = L > 0 ? L - 1 : 0;       // path entries before the last
             const int pr = __shfl_up(r, 1, 64), pd = __shfl_up(d, 1, 64);
             const bool head = valid && (lane == 0 || pr != r || pd != d);
@@ -626,28 +632,28 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
                     hipLaunchKernelGGL((route_seg_packed_kernel<1024, false, true, false>),
                                        dim3((unsigned)g), dim3(256), 0, ctx->stream, ctx->V, tree,
                                        tabs, d_rows, d_dsts, d_last_port, npairs, d_off,
-                                       reinterpret_cast<int32_t *>(d_entries), nullptr);
+                                       reinterpret_cast<int32_t *>(d_entries), nullptr, ctx->d_err);
                 else
                     hipLaunchKernelGGL((route_seg_packed_kernel<1024, false, true, true>),
                                        dim3((unsigned)g), dim3(256), 0, ctx->stream, ctx->V, tree,
                                        tabs, d_rows, d_dsts, d_last_port, npairs, d_off,
-                                       reinterpret_cast<int32_t *>(d_entries), nullptr);
+                                       reinterpret_cast<int32_t *>(d_entries), nullptr, ctx->d_err);
             } else {
                 ctx->last_kernel = "route_seg_packed_kernel<1024>";
                 if (nt && !strcmp(nt, "1"))
                     hipLaunchKernelGGL((route_seg_packed_kernel<1024, true, false>), dim3((unsigned)g),
                                        dim3(256), 0, ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts,
-                                       d_last_port, npairs, d_off, d_switch, d_hport);
+                                       d_last_port, npairs, d_off, d_switch, d_hport, nullptr);
                 else if ((((uintptr_t)d_switch ^ (uintptr_t)d_hport) & 15u) == 0 && !(v4 && !strcmp(v4, "0")))
                     // both arrays share their 16-B phase: 16-B stores into each
                     hipLaunchKernelGGL((route_seg_packed_kernel<1024, false, false, true>),
                                        dim3((unsigned)g), dim3(256), 0, ctx->stream, ctx->V, tree,
                                        tabs, d_rows, d_dsts, d_last_port, npairs, d_off, d_switch,
-                                       d_hport);
+                                       d_hport, nullptr);
                 else
                     hipLaunchKernelGGL((route_seg_packed_kernel<1024, false, false>), dim3((unsigned)g),
                                        dim3(256), 0, ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts,
-                                       d_last_port, npairs, d_off, d_switch, d_hport);
+                                       d_last_port, npairs, d_off, d_switch, d_hport, nullptr);
             }
         } else {
             int64_t g = ((int64_t)npairs * 16 + 255) / 256;

@@ -689,8 +689,13 @@ __global__ __launch_bounds__(256) void msbfs_plane_seed_kernel(
     uint64_t *b = pl + (size_t)(i >> 6) * npl * VS;
     atomicOr((unsigned long long *)&b[(size_t)kPlVis * VS + d], 1ull << (i & 63));
     atomicOr((unsigned long long *)&b[(size_t)kPlFront * VS + d], 1ull << (i & 63));
-    // a batch of one destination has its (batch, d) word complete already
-    if (ndst - (i & ~63) == 1) atomicAdd(full, 1);
+    // a batch whose destinations are all d (one destination, or repeats)
+    // has its (batch, d) word complete already
+    if ((i & 63) == 0) {
+        bool same = true;
+        for (int k = i + 1; same && k < min(ndst, i + 64); ++k) same = dst[k] == d;
+        if (same) atomicAdd(full, 1);
+    }
 }
 
 // the planes of a chunk zeroed, the destinations seeded into the visited and
@@ -725,11 +730,21 @@ __global__ __launch_bounds__(256) void msbfs_plane_init_kernel(
     if (batch == 0 && blockIdx.x == 0) {
         for (int i = threadIdx.x; i < nflags; i += blockDim.x) flags[i] = 0;
         __syncthreads();
-        // a last batch of one destination has its (batch, d) word complete
-        if (threadIdx.x == 0 && ndst - ((ndst - 1) & ~63) == 1) {
-            const int d = dst[ndst - 1];
-            if (d >= 0 && d < V) status[0] = 1;
+        // words complete from the start: a batch whose destinations are all
+        // one valid vertex d (a last batch of one destination, or repeats)
+        // has its (batch, d) word complete before level 1, and the level
+        // pass counts only words that become complete -- count these here,
+        // behind the reset, so the count still reaches V x batches
+        const int nbatch = (ndst + 63) >> 6;
+        int seeded = 0;
+        for (int bt = threadIdx.x; bt < nbatch; bt += blockDim.x) {
+            const int n0 = bt * 64, n1 = min(ndst, n0 + 64);
+            const int d = dst[n0];
+            bool same = d >= 0 && d < V;
+            for (int i = n0 + 1; same && i < n1; ++i) same = dst[i] == d;
+            seeded += same;
         }
+        if (seeded) atomicAdd(&status[0], seeded);
     }
 }
 

@@ -563,13 +563,16 @@ class _Pool(object):
             self.host.pop(v, None)
         if not slots:
             return
-        idx = np.asarray(slots, np.int64)
+        self._blank(np.asarray(slots, np.int64))
+        self.free.extend(slots)
+
+    def _blank(self, idx):
+        """Rows ``idx`` back to all-unreached (every free slot is blank)."""
         for a, b in zip(self.arrays, self.blanks):
             if _is_np(a):
                 a[idx] = b
             else:
                 a[_torch().as_tensor(idx, device=a.device)] = b
-        self.free.extend(slots)
 
     def add(self, verts, tabs=None, fill=None, like=None):
         """Store rows for ``verts`` (room was made): either ``tabs`` ([n, V]
@@ -593,7 +596,10 @@ class _Pool(object):
                     tabs = tuple(_empty_rows(a, n) for a in self.arrays)
                     fill(tabs)
             except BaseException:
-                self.free.extend(slots)            # nothing was stored
+                # the kernels may have written part of the rows in place:
+                # blank the slots before they go back
+                self._blank(idx)
+                self.free.extend(slots)
                 raise
         if tabs is not None:
             for a, t in zip(self.arrays, tabs):
@@ -802,7 +808,9 @@ class TableCache(object):
                 r, v = t.nonzero(need, as_tuple=True)
                 p = par[r, v]
                 k = p * V + v
-                e = t.searchsorted(xp_keys, k)
+                e = t.searchsorted(xp_keys, k).clamp_(max=xp_keys.shape[0] - 1)
+                if not bool((xp_keys[e] == k).all()):     # the kept tree edge must exist
+                    raise AssertionError("kept tree edge missing")
                 x[r, v] = p | ((xp_e[e] - xp_rp[p]) << 26)
                 x = t.where(x >= (1 << 31), x - (1 << 32), x).to(t.int32)
                 tree.index_copy_(0, t.as_tensor(sl, device=dv), x)

@@ -448,7 +448,7 @@ class TopologyDB(object):
             hp_all[pos] = hp
         return off, ex.csr.dpids[np.asarray(sw_all, np.int64)], hp_all
 
-    def switch_fdb_entries(self, pairs):
+    def switch_fdb_entries(self, pairs, keys=None):
         """The flow entries of many (src_mac, dst_mac) pairs grouped by switch
         -- what ``Router._add_flows_for_path`` records in ``SwitchFDB``
         (reference ``sdnmpi/router.py:83-104``, ``util/switch_fdb.py:6-9``:
@@ -461,8 +461,15 @@ class TopologyDB(object):
         pair ``pair[j]`` (index into ``pairs``) leaving on ``out_port[j]``;
         ``last[j]`` marks the pair's destination switch (where the router
         adds the SetDlDst action for an MPI flow, :97-100).  Switches ascend
-        by dpid, entries keep pair order within a switch."""
+        by dpid, entries keep pair order within a switch.
+
+        ``keys``: the SwitchFDB key of each pair when it is not the pair
+        itself -- an MPI flow is recorded under (src MAC, the virtual
+        destination MAC), ``router.py:189-193`` (see :meth:`mpi_flow_entries`)."""
         pairs = list(pairs)
+        keys = pairs if keys is None else list(keys)
+        if len(keys) != len(pairs):
+            raise ValueError("one SwitchFDB key per pair")
         off, dp, pt = self.route_entries(pairs)
         n = len(pairs)
         lens = np.diff(off)
@@ -471,8 +478,8 @@ class TopologyDB(object):
         ends = off[1:][lens > 0] - 1
         last[ends] = True
         # first occurrence of every (src, dst) key wins (SwitchFDB.exists)
-        keys = {}
-        first = np.fromiter((keys.setdefault(k, i) for i, k in enumerate(pairs)), np.int64, n)
+        seen = {}
+        first = np.fromiter((seen.setdefault(k, i) for i, k in enumerate(keys)), np.int64, n)
         keep = first[pid] == pid          # (routes are simple paths: one entry per switch)
         pid, dp, pt, last = pid[keep], np.asarray(dp)[keep], np.asarray(pt)[keep], last[keep]
         order = np.lexsort((np.arange(pid.shape[0]), dp))           # by dpid, stable
@@ -495,13 +502,17 @@ class TopologyDB(object):
         installs, per switch of ``find_route(mac_i, mac_j)``, a flow matching
         (src ``mac_i``, dst the virtual address ``sdn_mpi_mac(coll_type, i,
         j)``) whose last hop rewrites the destination to ``mac_j``
-        (``router.py:166-200``).  Returns ``(dpids, off, src_rank, dst_rank,
-        out_port, last)`` as :meth:`switch_fdb_entries` lays them out."""
+        (``router.py:166-200``).  The router records each flow in SwitchFDB
+        under (``mac_i``, virtual MAC), so ranks sharing a host keep one flow
+        per rank pair (``router.py:189-193``, ``switch_fdb.py:6-13``).
+        Returns ``(dpids, off, src_rank, dst_rank, out_port, last)`` as
+        :meth:`switch_fdb_entries` lays them out."""
         ranks = sorted(rank_to_mac)
         src_r = [a for a in ranks for b in ranks if a != b]
         dst_r = [b for a in ranks for b in ranks if a != b]
         pairs = [(rank_to_mac[a], rank_to_mac[b]) for a, b in zip(src_r, dst_r)]
-        dpids, off, pid, pt, last = self.switch_fdb_entries(pairs)
+        keys = [(rank_to_mac[a], sdn_mpi_mac(coll_type, a, b)) for a, b in zip(src_r, dst_r)]
+        dpids, off, pid, pt, last = self.switch_fdb_entries(pairs, keys)
         sr = np.asarray(src_r, np.int64)[pid] if pid.size else np.zeros(0, np.int64)
         dr = np.asarray(dst_r, np.int64)[pid] if pid.size else np.zeros(0, np.int64)
         return dpids, off, sr, dr, pt, last

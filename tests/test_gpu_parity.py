@@ -471,6 +471,45 @@ def test_shortest_plane_compact_levels(ctx, monkeypatch, dp):
         np.testing.assert_array_equal(nhp, nhpo)
 
 
+@pytest.mark.parametrize("init", ["init", "seed"])
+@pytest.mark.parametrize("dp", ["auto", "8"])
+def test_shortest_plane_repeated_destinations(ctx, monkeypatch, dp, init):
+    """Batches whose destinations are all one vertex ([5, 5], a full batch of
+    one id) or hold repeats and unknown ids, in compact and 8-plane mode,
+    with the one-launch init and the old fill + seed path: the complete-word
+    count must see the words complete from the start, and every
+    table stays bit-exact vs the oracle."""
+    monkeypatch.setenv("SDNROUTE_SP_STRATEGY", "plane")
+    if dp != "auto":
+        monkeypatch.setenv("SDNROUTE_PLANE_DP", dp)
+    if init == "seed":
+        monkeypatch.setenv("SDNROUTE_PLANE_INIT", "0")
+    import torch
+    csr = T.fat_tree(8).csr()
+    ctx.upload(csr)
+    V = csr.V
+    dev = torch.device("cuda", 0)
+    for dsts in ([5, 5], [7] * 64, [7] * 64 + [9] * 64 + [3], [3, 3, -1, 3],
+                 list(range(V)) + [11] * 70, [0, V + 5], [2, 2, 2, 2]):
+        dsts = np.asarray(dsts, np.int32)
+        n = dsts.shape[0]
+        td = torch.from_numpy(dsts).to(dev)       # device path: unknown ids give blank rows
+        dist = torch.zeros((n, V), dtype=torch.int16, device=dev)
+        nh = torch.zeros((n, V), dtype=torch.int32, device=dev)
+        nhp = torch.zeros_like(nh)
+        ctx.shortest_tables_device(td.data_ptr(), n, dist.data_ptr(), nh.data_ptr(),
+                                   nhp.data_ptr())
+        ctx.synchronize()
+        dist = dist.cpu().numpy().view(np.uint16)
+        nh, nhp = nh.cpu().numpy(), nhp.cpu().numpy()
+        ok = (dsts >= 0) & (dsts < V)
+        do, nho, nhpo = O.dest_tables(csr, dsts[ok], nthreads=NTHREADS)
+        np.testing.assert_array_equal(dist[ok], do)
+        np.testing.assert_array_equal(nh[ok], nho)
+        np.testing.assert_array_equal(nhp[ok], nhpo)
+        assert (dist[~ok] == 0xFFFF).all() and (nh[~ok] == -1).all()
+
+
 @pytest.mark.parametrize("strategy", ["auto", "msbfs", "plane", "lanes"])
 def test_shortest_fullsize_torus_sample(ctx, monkeypatch, strategy):
     """torus 32^3 (the BASELINE multi-source BFS config), spread destinations:
@@ -785,3 +824,38 @@ def test_shortest_plane_too_deep_falls_back(ctx, monkeypatch):
     np.testing.assert_array_equal(dist, do)
     np.testing.assert_array_equal(nh, nho)
     np.testing.assert_array_equal(nhp, nhpo)
+
+
+def test_route_expand_packed_rejects_wide_last_port(ctx):
+    """sdnr_route_expand_packed keeps a 16-bit port per u32 entry: a last
+    (host) port above 0xFFFF, or negative, fails the call (the device sets
+    the watchdog word; sdnr_synchronize reports EINVAL) instead of keeping
+    its low bits -- ADVICE r4.  In-range ports expand as before."""
+    import torch
+    csr = T.fat_tree(4).csr()
+    ctx.upload(csr)
+    dev = torch.device("cuda", 0)
+    srcs = np.arange(csr.V, dtype=np.int32)
+    par, prt, hop = O.dfs_tables(csr, srcs, nthreads=NTHREADS)
+    tp, tt, th = (torch.from_numpy(a).to(dev) for a in (par, prt, hop))
+    rows = torch.tensor([0, 1, 2], dtype=torch.int32, device=dev)
+    dsts = torch.tensor([5, 6, 7], dtype=torch.int32, device=dev)
+    off = torch.empty(4, dtype=torch.int64, device=dev)
+    ctx.route_offsets_device(th.data_ptr(), rows.data_ptr(), dsts.data_ptr(), 3, off.data_ptr(),
+                             nrows=csr.V)
+    ctx.synchronize()
+    ent = torch.zeros(int(off[-1].item()), dtype=torch.int32, device=dev)
+    for bad, ok in (([1, 70000, 2], False), ([1, -1, 2], False), ([1, 0xFFFE, 2], True)):
+        last = torch.tensor(bad, dtype=torch.int32, device=dev)
+        ctx.expand_routes_packed_device(tp.data_ptr(), tt.data_ptr(), csr.V, rows.data_ptr(),
+                                        dsts.data_ptr(), last.data_ptr(), 3, off.data_ptr(),
+                                        ent.data_ptr())
+        if ok:
+            ctx.synchronize()
+            o = off.cpu().numpy()
+            e = ent.cpu().numpy().view(np.uint32)
+            assert e[o[2] - 1] == 6 | (0xFFFE << 16)
+        else:
+            with pytest.raises(_native.SdnrError) as ei:
+                ctx.synchronize()
+            assert ei.value.code == -22 and "last port" in str(ei.value)

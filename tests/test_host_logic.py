@@ -149,3 +149,27 @@ def test_unpack_tree_layout():
     p, q = unpack_tree(t)
     assert p.tolist() == [[2, 5, -1, 0]]
     assert q.tolist() == [[3, -1, -1, 0xFFFE]]
+
+
+def test_pool_failed_fill_leaves_slots_blank():
+    """A fill that writes part of its rows in place and then raises gives
+    the slots back blank (free slots must stay all-unreached,
+    which drop() and the incremental row tests rely on)."""
+    from sdnmpi_amd.engine import _Pool
+    V = 8
+    pool = _Pool(budget=1 << 20, row_bytes=8 * V, blanks=(-1, -1))
+    like = (np.empty((0, V), np.int32), np.empty((0, V), np.int32))
+
+    def bad_fill(out):
+        out[0][...] = 7                      # partial in-place write, then a failure
+        raise RuntimeError("kernel failed")
+
+    with pytest.raises(RuntimeError):
+        pool.add([0, 1, 2], fill=bad_fill, like=like)
+    assert len(pool) == 0
+    assert all((a == -1).all() for a in pool.arrays)
+    pool.add([3, 4], fill=lambda out: [o.fill(5) for o in out], like=like)
+    rows = sorted(pool.row.values())
+    assert all((a[rows] == 5).all() for a in pool.arrays)
+    others = [i for i in range(pool.size) if i not in rows]
+    assert all((a[others] == -1).all() for a in pool.arrays)

@@ -657,6 +657,23 @@ def _switch_fdb_check(db, fabric, rng):
     want = _replay_switch_fdb(db, [(ranks[a], ranks[b]) for a, b in rp], keys=rp)
     got = _grouped_to_dict(dpids, off, list(zip(sr.tolist(), dr.tolist())), port)
     assert got == want
+    # several ranks per host (ranks take eth.src, process.py:108-109): the
+    # router keys each flow by (src MAC, virtual MAC), so rank pairs sharing
+    # both hosts still get one flow each (router.py:189-193)
+    from oracle import oracle as O
+    from sdnmpi_amd.util.topology_db import sdn_mpi_mac
+    hosts = rng.choice(len(macs), 4, replace=False)
+    ranks = {r: macs[int(hosts[r % 4])] for r in range(10)}
+    dpids, off, sr, dr, port, last = db.mpi_flow_entries(ranks, coll_type=2)
+    rp = [(a, b) for a in sorted(ranks) for b in sorted(ranks) if a != b]
+    keys = [(ranks[a], sdn_mpi_mac(2, a, b)) for a, b in rp]
+    want = _replay_switch_fdb(db, [(ranks[a], ranks[b]) for a, b in rp], keys=keys)
+    got = _grouped_to_dict(dpids, off, [(ranks[a], sdn_mpi_mac(2, a, b))
+                                        for a, b in zip(sr.tolist(), dr.tolist())], port)
+    assert got == want
+    assert sum(len(v) for v in got.values()) == int(off[-1])   # no pair's entries dropped
+    n_hops = sum(len(O.find_route_pair(db, ranks[a], ranks[b])) for a, b in rp)
+    assert int(off[-1]) == n_hops
 
 
 def test_switch_fdb_entries_fake_engine():
