@@ -154,6 +154,7 @@ int sdnr_dfs_tables_slots(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc,
  * pointers only (flags must hold SDNR_DEVICE_PTRS); asynchronous on the
  * context stream.  The route cache of the Python TopologyDB keeps its rows
  * in these layouts (a third of the int32 tables' bytes). */
+#define SDNR_TREE_INT32  0   /* int32 parents (sdnr_dfs_rows_affected only) */
 #define SDNR_TREE_PORT16 1
 #define SDNR_TREE_SLOT   2
 int sdnr_tree_pack(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port,
@@ -171,6 +172,30 @@ int sdnr_tree_pack(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port,
 int sdnr_dfs_tables_tree(sdnr_ctx *ctx, const int32_t *src, int32_t nsrc,
                          uint32_t *tree, void *depth, int32_t layout,
                          int32_t depth_bytes, uint32_t flags);
+
+/* Incremental recompute on link events: EventLinkAdd /
+ * EventLinkDelete -> TopologyDB.add_link / delete_link (reference
+ * sdnmpi/topology.py:192-198, sdnmpi/util/topology_db.py:30-42).  Which
+ * cached default-route rows a set of link changes alters, decided from the
+ * rows themselves: the tree words (layout SDNR_TREE_PORT16 / SDNR_TREE_SLOT
+ * as sdnr_dfs_tables_tree writes them, or SDNR_TREE_INT32: int32 parents)
+ * and depths (depth_bytes 2: u16, 0xFFFF unreached; 4: int32, -1) of
+ * [nrows][V] rows; row_src[r] = the source of row r (-1: a free row, never
+ * flagged).  links = (u, v) dense-id pairs: the first nremoved removed or
+ * re-ported links, then nadded added links (ids against the CURRENT graph's
+ * vertex set, which must equal the rows').  affected[r] = 1 iff the row
+ * changes (exact for one link change, a superset for several):
+ *   removed / re-ported (u, v): parent[v] == u;
+ *   added (u, v): u reached and v unreached, or v pushed in a pop after u's
+ *   (preorder, children in descending id order: the two root paths decide).
+ * Device pointers only (flags must hold SDNR_DEVICE_PTRS); asynchronous on
+ * the context stream; a row that is not a tree is reported by
+ * sdnr_synchronize as SDNR_ERR_INVAL. */
+int sdnr_dfs_rows_affected(sdnr_ctx *ctx, const uint32_t *tree, const void *depth,
+                           int32_t layout, int32_t depth_bytes, int32_t nrows,
+                           const int32_t *row_src, const int32_t *links,
+                           int32_t nremoved, int32_t nadded, uint8_t *affected,
+                           uint32_t flags);
 
 /* Shortest routes, find_route(src, dst, multiple=True) -> _find_routes_bfs
  * (topology_db.py:86-122, called from :168-180), as per-destination tables:

@@ -43,6 +43,10 @@ int sdnr_check_watchdog(sdnr_ctx *ctx)
     SDNR_HIP(hipMemcpy(&h, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (h) {
         SDNR_HIP(hipMemset(ctx->d_err, 0, sizeof(int)));
+        if (h == kErrTreeClimb)
+            return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_rows_affected: a tree row is not a tree "
+                             "(a parent chain longer than V, or a reached vertex without a "
+                             "reached parent)");
         if (h == kErrLastPort)
             return sdnr_fail(SDNR_ERR_INVAL, "sdnr_route_expand_packed: a last port outside "
                              "[0, 0xFFFF] (u32 entries hold 16-bit ports): entries invalid");
@@ -969,6 +973,34 @@ int sdnr_tree_pack(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port, in
     if (n == 0 || ctx->V == 0) return SDNR_OK;
     SDNR_HIP(hipSetDevice(ctx->device));
     return sdnr_launch_tree_pack(ctx, parent, port, (size_t)n, tree, layout == SDNR_TREE_SLOT);
+}
+
+int sdnr_dfs_rows_affected(sdnr_ctx *ctx, const uint32_t *tree, const void *depth, int32_t layout,
+                           int32_t depth_bytes, int32_t nrows, const int32_t *row_src,
+                           const int32_t *links, int32_t nremoved, int32_t nadded,
+                           uint8_t *affected, uint32_t flags)
+{
+    CHECK_CTX(ctx);
+    if (ctx->V < 0) return sdnr_fail(SDNR_ERR_STATE, "sdnr_dfs_rows_affected: no graph uploaded");
+    if (!(flags & SDNR_DEVICE_PTRS))
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_rows_affected: device pointers only");
+    if (nrows < 0 || nremoved < 0 || nadded < 0)
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_rows_affected: negative count");
+    if (layout != SDNR_TREE_INT32 && layout != SDNR_TREE_PORT16 && layout != SDNR_TREE_SLOT)
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_rows_affected: layout %d", layout);
+    if (depth_bytes != 2 && depth_bytes != 4)
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_rows_affected: depth_bytes %d", depth_bytes);
+    if (depth_bytes == 2 && ctx->V > 0xFFFF)
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_rows_affected: u16 depths need V <= 65535");
+    if (nrows > 0 && (!tree || !depth || !row_src || !affected))
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_rows_affected: null table");
+    if (nremoved + nadded > 0 && !links)
+        return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_rows_affected: null links");
+    if (nrows == 0) return SDNR_OK;
+    SDNR_HIP(hipSetDevice(ctx->device));
+    ctx->timed = (flags & SDNR_TIMING) != 0;
+    return sdnr_launch_dfs_rows_affected(ctx, tree, depth, layout, depth_bytes, nrows, row_src,
+                                         links, nremoved, nadded, affected);
 }
 
 int sdnr_shortest_tables(sdnr_ctx *ctx, const int32_t *dst, int32_t ndst, uint16_t *dist,

@@ -123,6 +123,7 @@ inline void sdnr_allow_lds(const void *fn, size_t bytes)
 // bounded waits that ran out); sdnr_synchronize turns a nonzero word into an
 // error
 constexpr int kErrLastPort = 256;   // sdnr_route_expand_packed: a last port outside [0, 0xFFFF]
+constexpr int kErrTreeClimb = 512;  // sdnr_dfs_rows_affected: a tree climb outran V steps
 
 // error plumbing (capi.hip)
 int sdnr_fail(int code, const char *fmt, ...);
@@ -179,5 +180,10 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
                              int32_t nrows, const int32_t *d_rows, const int32_t *d_dsts,
                              const int32_t *d_last_port, int32_t npairs, const int64_t *d_off,
                              int32_t *d_switch, int32_t *d_hport, uint32_t *d_entries = nullptr);
+// rows of cached default-route trees a link change alters (incremental.hip)
+int sdnr_launch_dfs_rows_affected(sdnr_ctx *ctx, const uint32_t *d_tree, const void *d_depth,
+                                  int32_t layout, int32_t depth_bytes, int32_t nrows,
+                                  const int32_t *d_row_src, const int32_t *d_links, int32_t nrm,
+                                  int32_t nadd, uint8_t *d_affected);
 int sdnr_launch_edge_ports(sdnr_ctx *ctx, const uint64_t *d_ends, int32_t nends,
                            const uint64_t *d_ports, int32_t nports, uint8_t *d_is_edge);

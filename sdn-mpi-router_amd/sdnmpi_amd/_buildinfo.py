@@ -19,7 +19,8 @@ INCLUDE = os.path.join(os.path.dirname(PKG), "include")
 
 # the product library: the kernels the route calls select, and nothing else
 # (losing variants live under tools/diag/)
-SOURCES = ("capi.hip", "dfs.hip", "shortest.hip", "apsp.hip", "routes.hip", "ecmp.hip")
+SOURCES = ("capi.hip", "dfs.hip", "shortest.hip", "apsp.hip", "routes.hip", "ecmp.hip",
+           "incremental.hip")
 HEADERS = (("csrc", "common.h"), ("include", "sdnroute.h"))
 FLAGS = ("--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function")
 MARKER = b"SDNR_BUILD_ID:"

@@ -27,6 +27,7 @@ TIMING = 0x2
 UNREACHED = -1
 DIST_INF = 0xFFFF
 TREE_NONE = 0xFFFFFFFF
+TREE_INT32 = 0           # int32 parents (sdnr_dfs_rows_affected)
 TREE_PORT16 = 1          # parent | port << 16 (sdnr_dfs_tables_packed)
 TREE_SLOT = 2            # parent | slot << 26 (sdnr_dfs_tables_slots)
 ABI_VERSION = 1
@@ -40,7 +41,7 @@ EXPORTED_SYMBOLS = (
     "sdnr_apsp", "sdnr_route_offsets", "sdnr_route_expand", "sdnr_ecmp_counts",
     "sdnr_ecmp_routes",
     "sdnr_last_kernel_ms", "sdnr_last_kernel", "sdnr_last_launches", "sdnr_last_sweeps",
-    "sdnr_edge_ports",
+    "sdnr_edge_ports", "sdnr_dfs_rows_affected",
 )
 
 
@@ -95,6 +96,7 @@ def _bind(L):
         "sdnr_last_launches": ([vp, ctypes.POINTER(i32)], c_int),
         "sdnr_last_sweeps": ([vp, ctypes.POINTER(i32)], c_int),
         "sdnr_edge_ports": ([vp, vp, i32, vp, i32, vp, u32], c_int),
+        "sdnr_dfs_rows_affected": ([vp, vp, vp, i32, i32, i32, vp, vp, i32, i32, vp, u32], c_int),
     }
     # an A/B build named by SDNROUTE_LIB may predate some entry points: those
     # stay unbound (calling one raises AttributeError); the in-tree library
@@ -397,6 +399,18 @@ class Context(object):
         _check(self._lib.sdnr_edge_ports(self._h, _ptr(ends), int(ends.shape[0]), _ptr(ports),
                                          int(ports.shape[0]), _ptr(out), 0))
         return out.astype(bool)
+
+    def dfs_rows_affected_device(self, tree_ptr, depth_ptr, layout, depth_bytes, nrows,
+                                 row_src_ptr, links_ptr, nremoved, nadded, affected_ptr,
+                                 timing=False):
+        """uint8 verdicts: which [nrows][V] tree rows the link changes alter
+        (sdnr_dfs_rows_affected, device pointers, asynchronous)."""
+        flags = DEVICE_PTRS | (TIMING if timing else 0)
+        _check(self._lib.sdnr_dfs_rows_affected(
+            self._h, ctypes.c_void_p(tree_ptr), ctypes.c_void_p(depth_ptr), int(layout),
+            int(depth_bytes), int(nrows), ctypes.c_void_p(row_src_ptr),
+            ctypes.c_void_p(links_ptr) if links_ptr else None, int(nremoved), int(nadded),
+            ctypes.c_void_p(affected_ptr), flags))
 
     def apsp(self):
         dist = np.empty((self.V, self.V), np.uint16)

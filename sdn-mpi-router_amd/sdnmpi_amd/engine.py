@@ -465,6 +465,34 @@ class RouteEngine(object):
         self.ctx.synchronize()
         return off, sw[:total].cpu().numpy(), hp[:total].cpu().numpy()
 
+    def dfs_rows_affected(self, export, tree, depth, layout, row_src, diff):
+        """bool numpy [rows]: the pool rows (device tree words / int32
+        parents ``tree`` and depths ``depth``, [rows, V]; ``row_src`` the
+        source of each row, -1 for a free one) that the link changes of
+        ``diff`` alter -- one device pass (sdnr_dfs_rows_affected), only
+        the verdicts come back."""
+        self.load(export)
+        t = self._torch
+        n = int(tree.shape[0])
+        rm = [np.concatenate([diff.removed[0], diff.ported[0]]),
+              np.concatenate([diff.removed[1], diff.ported[1]])]
+        links = np.concatenate([np.stack(rm, 1).reshape(-1),
+                                np.stack([diff.added[0], diff.added[1]], 1).reshape(-1)])
+        nrm, nadd = int(rm[0].size), int(diff.added[0].size)
+        if n == 0 or nrm + nadd == 0:
+            return np.zeros(n, bool)
+        tl = self._torch.from_numpy(links.astype(np.int32)).to(self.dev)
+        ts = self._ids(row_src)
+        out = t.empty(n, dtype=t.uint8, device=self.dev)
+        lay = {PORT16: _native.TREE_PORT16, SLOT: _native.TREE_SLOT,
+               INT32: _native.TREE_INT32}[layout]
+        self._ready()
+        self.ctx.dfs_rows_affected_device(tree.data_ptr(), depth.data_ptr(), lay,
+                                          depth.element_size(), n, ts.data_ptr(),
+                                          tl.data_ptr(), nrm, nadd, out.data_ptr())
+        self.ctx.synchronize()              # raises if a row was not a tree
+        return out.cpu().numpy().astype(bool)
+
     def edge_ports(self, ends, ports):
         """Flood-port mask (sdnr_edge_ports, reference topology.py:150-155):
         bool [n] -- ``ports`` keys that are no link end (``ends`` sorted)."""
@@ -721,7 +749,7 @@ class TableCache(object):
                 _host(nhp).astype(np.int32))
 
     # -- graph changes ---------------------------------------------------
-    def retarget(self, export, diff):
+    def retarget(self, export, diff, engine=None):
         """Follow a link change over the same vertex set: drop the rows
         ``diff`` can alter (tests run where the tables live), keep the rest.
         Returns False when the compact layout no longer fits the new graph
@@ -731,9 +759,15 @@ class TableCache(object):
             return False
         self.export = export
         if self.dfs.row:
-            par, hop = self.dfs_parent_hops()
             verts = self.dfs.slot_vertices()
-            hit = np.asarray(dfs_rows_affected(par, hop, verts, diff), bool) & (verts >= 0)
+            a = self.dfs.tables()
+            if engine is not None and not _is_np(a[0]):
+                # the device pool: one kernel climbs the trees (incremental.hip)
+                hit = engine.dfs_rows_affected(export, a[0], a[-1], self.layout, verts, diff)
+            else:
+                par, hop = self.dfs_parent_hops()
+                hit = np.asarray(dfs_rows_affected(par, hop, verts, diff), bool)
+            hit &= verts >= 0
             self.dfs.drop(verts[hit].tolist())
             if self.layout == SLOT:
                 self._reslot(diff)

@@ -168,7 +168,7 @@ class TopologyDB(object):
         old = self._cache
         self._export = new
         if not (self._incremental and old is not None and diff is not None and
-                old.retarget(new, diff)):
+                old.retarget(new, diff, self._engine)):
             self._cache = TableCache(new, self._budget)
         return new
 
