@@ -1063,6 +1063,82 @@ constexpr int kFlagPreSwz = 16;
 // hop counts written as u16 (0xFFFF unreached) instead of int32: the depth
 // plane of the drop-in's table pool (sdnr_dfs_tables_tree)
 constexpr int kFlagHops16 = 32;
+// split kernel: sources taken from the CU's own contiguous chunk (see
+// split_next_source) instead of the static blockIdx-strided order
+constexpr int kFlagCuMap = 64;
+
+// s_getreg encodings: (size - 1) << 11 | offset << 6 | register id
+constexpr int kHwIdReg = (31 << 11) | 4;      // HW_REG_HW_ID: cu [11:8], sh [12], se [14:13]
+constexpr int kXccIdReg = (15 << 11) | 20;    // HW_REG_XCC_ID: the XCD
+
+// Number of this wave's CU, 0, 1, 2, ... in order of first arrival (wq:
+// [nch] chunk cursors | arrivals counter | 1,024-entry CU table, -1 = not
+// numbered yet, -2 = being numbered).  Lane 0 works; the result is uniform.
+__device__ int split_cu_number(int *wq, int nch, int lane, int *err)
+{
+    const uint32_t hw = __builtin_amdgcn_s_getreg(kHwIdReg);
+    const uint32_t xcc = __builtin_amdgcn_s_getreg(kXccIdReg) & 7u;
+    const int key = (int)((((xcc * 4u + ((hw >> 13) & 3u)) * 2u + ((hw >> 12) & 1u)) * 16u) +
+                          ((hw >> 8) & 15u));
+    int *tab = wq + nch + 1;
+    int n = 0;
+    if (lane == 0) {
+        int v = atomicCAS(&tab[key], -1, -2);
+        if (v == -1) {
+            n = atomicAdd(&wq[nch], 1);
+            __hip_atomic_store(&tab[key], n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            for (unsigned spin = 0; v < 0; ++spin) {
+                if (spin > (1u << 22)) {
+                    atomicOr(err, 32);
+                    v = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                v = __hip_atomic_load(&tab[key], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            n = v;
+        }
+    }
+    return uniform(read_lane(n, 0)) % nch;
+}
+
+// The next source of a search wave under kFlagCuMap: the sources are cut
+// into nch contiguous chunks, one per CU (by arrival number); a wave takes
+// the next source of its chunk, so the ~28 search waves co-resident on a CU
+// walk neighbouring sources at the same time (on the torus their traversals
+// read neighbouring rows, which the CU's L1 then serves).  A
+// wave whose chunk is exhausted looks 64 chunks at a time for one with
+// sources left (cursor loads at agent scope) and takes from it.  Returns
+// nsrc when no chunk has work.  Bounded: every failed claim exhausts a chunk.
+__device__ int split_next_source(int *wq, int nch, int nsrc, int *chunk, int lane)
+{
+    for (int guard = 0; guard <= 2 * nch + 2; ++guard) {
+        const int c = *chunk;
+        const int lo = (int)((int64_t)c * nsrc / nch), hi = (int)((int64_t)(c + 1) * nsrc / nch);
+        int t = 0;
+        if (lane == 0) t = atomicAdd(&wq[c], 1);
+        t = uniform(read_lane(t, 0));
+        if (lo + t < hi) return lo + t;
+        int found = -1;
+        for (int base = 0; base < nch && found < 0; base += SDNR_WAVE) {
+            const int k = base + lane;
+            bool has = false;
+            int cc = 0;
+            if (k < nch) {
+                cc = c + 1 + k < nch ? c + 1 + k : c + 1 + k - nch;
+                const int l2 = (int)((int64_t)cc * nsrc / nch);
+                const int h2 = (int)((int64_t)(cc + 1) * nsrc / nch);
+                has = l2 + __hip_atomic_load(&wq[cc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < h2;
+            }
+            const uint64_t m = __ballot(has);
+            if (m) found = read_lane(cc, __ffsll((unsigned long long)m) - 1);
+        }
+        if (found < 0) return nsrc;
+        *chunk = found;
+    }
+    return nsrc;
+}
 
 // hop count of entry e of an [rows][V] hop table, int32 or u16 (kFlagHops16)
 __device__ __forceinline__ void put_hop(int32_t *__restrict__ hops, size_t e, int h, int flags)
@@ -1227,7 +1303,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
     const int32_t *__restrict__ ell_port, const int32_t *__restrict__ src, int nsrc,
     int32_t *__restrict__ out_parent, int32_t *__restrict__ out_port,
     int32_t *__restrict__ out_hops, uint2 *__restrict__ spill_all, int *__restrict__ err,
-    int flags)
+    int flags, int *__restrict__ wq, int nch)
 {
     constexpr int R = 64 / LPR;
     constexpr int K = R * J;
@@ -1270,7 +1346,14 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                                                    z_nl = 0, z_sp = 0, z_rf = 0, z_rfc = 0;
         SDNR_STAMP(z_t0);
 #endif
-        for (int si = slot_id; si < nsrc; si += gridDim.x * NS) {
+        // source order: blockIdx-strided, or (kFlagCuMap) the CU's own chunk
+        const bool cumap = (flags & kFlagCuMap) != 0;
+        int chunk = cumap ? split_cu_number(wq, nch, lane, err) : 0;
+        auto next_source = [&](int prev) -> int {
+            if (!cumap) return prev < 0 ? slot_id : prev + (int)gridDim.x * NS;
+            return split_next_source(wq, nch, nsrc, &chunk, lane);
+        };
+        for (int si = next_source(-1); si < nsrc; si = next_source(si)) {
             const int s = uniform(src[si]);
             int32_t *prow = out_parent + (size_t)si * V;
             int32_t *trow = PACKED ? nullptr : out_port + (size_t)si * V;
@@ -2350,14 +2433,27 @@ static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, in
     // rows of 9-16 slots (Jellyfish): search waves issue at raised priority
     // over their writer (measured 1.027 -> 0.973 s on the 100k Jellyfish; the
     // torus rows of 6 slots measured 3 % slower with it, so not there)
-    const int flags = dfs_flags(lpr == 16 ? kFlagPrio : 0) | hflags;
+    int flags = dfs_flags(lpr == 16 ? kFlagPrio : 0) | hflags;
+    // sources by CU chunk (kFlagCuMap; SDNROUTE_DFS_CUMAP=0|1 overrides)
+    bool cumap = false;
+    if (const char *f = getenv("SDNROUTE_DFS_CUMAP")) cumap = !strcmp(f, "1");
+    const int nch = ctx->num_cus;
+    int *wq = nullptr;
+    if (cumap) {
+        flags |= kFlagCuMap;
+        rc = sdnr_reserve(&ctx->wq, &ctx->wq_bytes, (size_t)(nch + 1 + 1024) * sizeof(int));
+        if (rc) return rc;
+        wq = static_cast<int *>(ctx->wq);
+        SDNR_HIP(hipMemsetAsync(wq, 0, (size_t)(nch + 1) * sizeof(int), ctx->stream));
+        SDNR_HIP(hipMemsetAsync(wq + nch + 1, 0xFF, 1024 * sizeof(int), ctx->stream));
+    }
 #define SDNR_SPLIT(L_, J_, R_, H_, F_, P_)                                                    \
     do {                                                                                     \
         auto k = dfs_split_kernel<L_, J_, H_, R_, NS, F_, P_>;                               \
         sdnr_allow_lds(reinterpret_cast<const void *>(k), lds);                              \
         hipLaunchKernelGGL(k, dim3(grid), dim3((NS + 1) * 64), lds, ctx->stream, V, W, rows,     \
                            ctx->ell_hi, ctx->ell_port, d_src, nsrc, par, d_port, d_hops,     \
-                           spill, ctx->d_err, flags);                                        \
+                           spill, ctx->d_err, flags, wq, nch);                               \
     } while (0)
 #define SDNR_SPLIT_F(L_, J_, R_, H_)                                                          \
     do {                                                                                     \

@@ -38,6 +38,9 @@ def _strategy(monkeypatch, dfs=None, ell=None):
     if dfs == "global-nosplit":                  # single-wave lane-packed kernel
         monkeypatch.setenv("SDNROUTE_DFS_SPLIT", "0")
         dfs = "global"
+    if dfs == "global-cumap":                    # split kernel, sources by CU chunk
+        monkeypatch.setenv("SDNROUTE_DFS_CUMAP", "1")
+        dfs = "global"
     if dfs:
         monkeypatch.setenv("SDNROUTE_DFS_STRATEGY", dfs)
     if ell is not None:
@@ -67,7 +70,8 @@ def _check_pairs(g, fabric, p, t, srcs):
 
 
 @pytest.mark.parametrize("strategy", ["auto", "async", "count", "coop", "lds", "global",
-                                      "global-ring128", "global-nopack", "global-nosplit"])
+                                      "global-ring128", "global-nopack", "global-nosplit",
+                                      "global-cumap"])
 @pytest.mark.parametrize("ell", [True, False])
 @pytest.mark.parametrize("name", G.SMALL)
 def test_dfs_small_all_sources(ctx, monkeypatch, name, strategy, ell):
@@ -118,7 +122,8 @@ def _expected_slots(csr, po):
     return want.astype(np.uint32)
 
 
-@pytest.mark.parametrize("strategy", ["auto", "async", "lds", "global", "global-nosplit"])
+@pytest.mark.parametrize("strategy", ["auto", "async", "lds", "global", "global-nosplit",
+                                      "global-cumap"])
 @pytest.mark.parametrize("name", ["mock", "fat_tree_k8", "dragonfly_a4_h2_p2", "random_V40",
                                   "jellyfish_n60_r5", "torus_5x3x2", "random_V60_dense"])
 def test_dfs_slots_small(ctx, monkeypatch, name, strategy):
@@ -278,11 +283,14 @@ def test_dfs_fullsize_all_host_sources(ctx, name):
     _check_pairs(g, fabric, p, t, srcs)
 
 
-@pytest.mark.parametrize("split", ["1", "0", "ns3", "ns7", "ns5", "ns5-ring256", "ns11-ring256"])
+@pytest.mark.parametrize("split", ["1", "0", "ns3", "ns7", "ns5", "ns5-ring256", "ns11-ring256",
+                                   "cumap0", "cumap1"])
 @pytest.mark.parametrize("name,nsample", [("torus_32x32x32_sample", 384),
                                           ("jellyfish_n100000_r16_sample", 48)])
 def test_dfs_fullsize_sampled_sources(ctx, monkeypatch, name, nsample, split):
-    if split.startswith("ns"):                   # search waves per workgroup
+    if split.startswith("cumap"):                # sources by CU chunk or strided
+        monkeypatch.setenv("SDNROUTE_DFS_CUMAP", split[-1])
+    elif split.startswith("ns"):                 # search waves per workgroup
         ns, _, ring = split[2:].partition("-ring")
         monkeypatch.setenv("SDNROUTE_DFS_SPLIT_NS", ns)
         if ring:
