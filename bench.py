@@ -66,6 +66,10 @@ def parse():
     ap.add_argument("--max-sources", type=int, default=0,
                     help="dfs/shortest: only the first N sources/destinations (probes; the "
                          "config then says so and value counts only their routes)")
+    ap.add_argument("--all-vertices", action="store_true",
+                    help="dfs/shortest: every switch as a source/destination (V x V switch "
+                         "pairs, e.g. route_tables('shortest', vertices=all)) instead of the "
+                         "host-bearing ones; value counts switch pairs")
     ap.add_argument("--event-every", type=int, default=4,
                     help="bracket every k-th timed launch with HIP events (kernel time; "
                          "the events themselves cost a few us per step)")
@@ -863,6 +867,8 @@ def main():
     srcs, counts = np.unique(hv, return_counts=True)
     srcs = srcs.astype(np.int32)
     H = fabric.n_hosts
+    if args.all_vertices:                   # switch pairs: one endpoint per switch
+        srcs, counts, H = np.arange(V, dtype=np.int32), np.ones(V, np.int64), V
     if args.max_sources and args.max_sources < len(srcs):
         pick = np.linspace(0, len(srcs) - 1, args.max_sources).astype(np.int64)
         srcs, counts = srcs[pick], counts[pick]
@@ -1003,7 +1009,10 @@ def main():
                 "" if args.mode == "dfs" else "(multiple=True)[0] + dist"),
             "fabric": args.fabric, "V": V, "E": E, "hosts": H, "sources": S,
             "host_pairs_per_step": int(routes), "table_layout": layout,
-            "source_subset": bool(args.max_sources and S < len(np.unique(hv))),
+            "endpoints": "every switch (V x V switch pairs)" if args.all_vertices
+                         else "host-bearing switches (host pairs)",
+            "source_subset": bool(args.max_sources and S < (V if args.all_vertices
+                                                             else len(np.unique(hv)))),
             "parallelism": "sources sharded over %d GPU(s)%s" % (
                 world, " + RCCL all-gather of the tables (double-buffered: step i+1's "
                        "kernel overlaps step i's gather)" if world > 1 else ""),
@@ -1053,14 +1062,14 @@ def main():
     # fat-trees only: their default routes are ~70 entries; a torus or
     # Jellyfish all-pairs fdb set (~2,400-5,600 entries per pair) is TBs
     if rank == 0 and world == 1 and args.mode == "dfs" and not args.max_sources and \
-            not args.no_flows and args.fabric.startswith("fat_tree"):
+            not args.no_flows and not args.all_vertices and args.fabric.startswith("fat_tree"):
         # the form the drop-in uses: one u32 word (switch | port << 16) per
         # entry, 4 B; the two int32 arrays (8 B per entry) beside it
         out["materialised_flows"] = materialised_flows(ctx, dev, stream, csr, fabric, srcs,
                                                        packed=True)
         out["materialised_flows_int32"] = materialised_flows(ctx, dev, stream, csr, fabric, srcs)
     if rank == 0 and world == 1 and args.mode == "dfs" and not args.max_sources and \
-            not args.no_flows and args.fabric.startswith("fat_tree"):
+            not args.no_flows and not args.all_vertices and args.fabric.startswith("fat_tree"):
         out["dropin"] = dropin_block(fabric)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "dfs":
         base, ref, ref_pred = cpu_baseline(fabric, csr, srcs, counts, H, args.cpu_budget_s)

@@ -963,6 +963,109 @@ __global__ __launch_bounds__(TB * Q) void msbfs_plane_tables_kernel(
 }  // namespace
 
 // SDNROUTE_SP_STRATEGY=msbfs|lanes forces the shortest-mode kernel (tests)
+// Shortest tables from all-pairs distances (SDNROUTE_SP_STRATEGY=apsp, and
+// the default where it measured faster): D = the min-plus APSP of apsp.hip
+// (D[a][b] = hops a -> b), then per requested destination d and vertex x
+//   dist[i][x] = D[x][d]   (row d of D when every link has its reverse),
+//   nh[i][x]   = the smallest out-neighbour n of x with D[n][d] = D[x][d] - 1,
+//   nh_port    = links[x][nh].src.port_no,
+// the same values as the BFS tables (the lexicographic rule of
+// _find_routes_bfs, reference sdnmpi/util/topology_db.py:86-122).  One
+// thread per (vertex, destination); the ELL row of x is scanned in slot
+// (= ascending id) order.  SYM: read row d of D (coalesced) instead of
+// column d.
+template <bool SYM>
+__global__ __launch_bounds__(256) void sp_from_apsp_kernel(
+    int V, int W, const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+    const int32_t *__restrict__ port, const int32_t *__restrict__ ell_col,
+    const int32_t *__restrict__ ell_port, const uint16_t *__restrict__ D,
+    const int32_t *__restrict__ dst, int ndst, uint16_t *__restrict__ dist,
+    int32_t *__restrict__ nh, int32_t *__restrict__ nh_port)
+{
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y;
+    if (x >= V || i >= ndst) return;
+    const int d = dst[i];
+    const size_t o = (size_t)i * V + x;
+    if (d < 0 || d >= V) {                      // unknown destination: blank row
+        dist[o] = 0xFFFF;
+        if (nh) {
+            nh[o] = -1;
+            nh_port[o] = -1;
+        }
+        return;
+    }
+    auto at = [&](int a) -> uint32_t {          // hops a -> d
+        return SYM ? D[(size_t)d * V + a] : D[(size_t)a * V + d];
+    };
+    const uint32_t dx = at(x);
+    dist[o] = (uint16_t)dx;
+    if (!nh) return;
+    int best = -1, bp = -1;
+    if (dx != 0u && dx != 0xFFFFu) {
+        if (W > 0) {
+            for (int j = 0; j < W; ++j) {
+                const int n = ell_col[(size_t)x * W + j];
+                if (n < 0) break;                   // -1 padding ends the row
+                if (at(n) == dx - 1u) {
+                    best = n;
+                    bp = ell_port[(size_t)x * W + j];
+                    break;
+                }
+            }
+        } else {
+            for (int e = row_ptr[x]; e < row_ptr[x + 1]; ++e)
+                if (at(col[e]) == dx - 1u) {
+                    best = col[e];
+                    bp = port[e];
+                    break;
+                }
+        }
+    }
+    nh[o] = best;
+    nh_port[o] = bp;
+}
+
+static int launch_sp_apsp(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uint16_t *d_dist,
+                          int32_t *d_nh, int32_t *d_nh_port)
+{
+    const int V = ctx->V;
+    // D lives in scratch2 (the APSP itself pads into scratch when V is not
+    // a multiple of its tile)
+    int rc = sdnr_reserve(&ctx->scratch2, &ctx->scratch2_bytes, (size_t)V * V * sizeof(uint16_t));
+    if (rc) return rc;
+    uint16_t *D = static_cast<uint16_t *>(ctx->scratch2);
+    const bool timed = ctx->timed;
+    ctx->timed = false;                          // the caller's events bracket both parts
+    rc = sdnr_launch_apsp(ctx, D);
+    ctx->timed = timed;
+    if (rc) return rc;
+    const dim3 grid((V + 255) / 256, ndst);
+    if (ctx->symmetric)
+        hipLaunchKernelGGL(sp_from_apsp_kernel<true>, grid, dim3(256), 0, ctx->stream, V, ctx->W,
+                           ctx->row_ptr, ctx->col, ctx->port, ctx->ell_col, ctx->ell_port, D,
+                           d_dst, ndst, d_dist, d_nh, d_nh_port);
+    else
+        hipLaunchKernelGGL(sp_from_apsp_kernel<false>, grid, dim3(256), 0, ctx->stream, V, ctx->W,
+                           ctx->row_ptr, ctx->col, ctx->port, ctx->ell_col, ctx->ell_port, D,
+                           d_dst, ndst, d_dist, d_nh, d_nh_port);
+    SDNR_HIP(hipGetLastError());
+    ctx->last_kernel = "apsp+sp_from_apsp_kernel";
+    if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+    return SDNR_OK;
+}
+
+// the APSP route to the shortest tables pays V^2 distances whatever the
+// destination count: only worth it for many destinations of a small graph
+// (SDNROUTE_SP_APSP=0|1 overrides the measured rule)
+static bool sp_apsp_default(const sdnr_ctx *ctx, int32_t ndst)
+{
+    if (const char *f = getenv("SDNROUTE_SP_APSP")) return !strcmp(f, "1");
+    (void)ctx;
+    (void)ndst;
+    return false;
+}
+
 static const char *sp_strategy()
 {
     const char *f = getenv("SDNROUTE_SP_STRATEGY");
@@ -1186,6 +1289,9 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
     // SDNROUTE_SP_STRATEGY=plane|lanes|msbfs forces a kernel family
     // rows of up to 64 slots: k=48 fat-tree (48 slots, 6 slot planes) 0.193 ->
     // 0.127 ms over bfs_dest_kernel, bit-exact
+    const bool apsp_ok = V <= 4096;
+    if (apsp_ok && (!strcmp(force, "apsp") || (!*force && sp_apsp_default(ctx, ndst))))
+        return launch_sp_apsp(ctx, d_dst, ndst, d_dist, d_nh, d_nh_port);
     const bool plane_ok = ctx->W > 0 && ctx->W <= 64;
     const bool plane_big = (size_t)ndst * (size_t)V >= ((size_t)1 << 21);
     if (plane_ok && (!strcmp(force, "plane") || (!*force && plane_big))) {

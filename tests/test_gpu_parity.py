@@ -337,9 +337,12 @@ def test_dfs_fullsize_tree_properties(ctx):
 
 
 @pytest.mark.parametrize("strategy", ["auto", "msbfs", "lanes", "lanes-csr", "plane",
-                                      "plane-opt0", "plane-opt2"])
+                                      "plane-opt0", "plane-opt2", "apsp", "apsp-csr"])
 @pytest.mark.parametrize("name", G.SMALL)
 def test_shortest_small_all_destinations(ctx, monkeypatch, name, strategy):
+    if strategy == "apsp-csr":                   # next hops from CSR rows (no ELL copy)
+        monkeypatch.setenv("SDNROUTE_ELL", "0")
+        strategy = "apsp"
     if strategy == "lanes-csr":                  # no ELL copy: 64-wide rows + CSR ports
         monkeypatch.setenv("SDNROUTE_ELL", "0")
         strategy = "lanes"
@@ -357,6 +360,44 @@ def test_shortest_small_all_destinations(ctx, monkeypatch, name, strategy):
     np.testing.assert_array_equal(dist, do)
     np.testing.assert_array_equal(nh, nho)
     np.testing.assert_array_equal(nhp, nhpo)
+
+
+@pytest.mark.parametrize("dsts", ["all", "hosts", "mixed"])
+@pytest.mark.parametrize("fab", ["fat_tree:48", "dragonfly:16,8,8", "fat_tree:8"])
+def test_shortest_tables_from_apsp(ctx, monkeypatch, fab, dsts):
+    """route_tables('shortest') through the APSP distances + next-hop
+    extraction (SDNROUTE_SP_STRATEGY=apsp) equals the oracle's BFS tables:
+    every vertex as a destination, the host switches, and a mixed list with
+    repeats and an unknown id (device path)."""
+    import torch
+    monkeypatch.setenv("SDNROUTE_SP_STRATEGY", "apsp")
+    fabric = T.by_name(fab)
+    csr = fabric.csr()
+    V = csr.V
+    if dsts == "all":
+        d = np.arange(V, dtype=np.int32)
+    elif dsts == "hosts":
+        d = np.unique(fabric.host_table()[0]).astype(np.int32)
+    else:
+        d = np.array([3, V - 1, 3, -1, 0, V // 2], np.int32)
+    ctx.upload(csr)
+    dev = torch.device("cuda", 0)
+    td = torch.from_numpy(d).to(dev)
+    dist = torch.empty((len(d), V), dtype=torch.int16, device=dev)
+    nh = torch.empty((len(d), V), dtype=torch.int32, device=dev)
+    nhp = torch.empty_like(nh)
+    ctx.shortest_tables_device(td.data_ptr(), len(d), dist.data_ptr(), nh.data_ptr(),
+                               nhp.data_ptr())
+    ctx.synchronize()
+    assert ctx.last_kernel() == "apsp+sp_from_apsp_kernel"
+    dist = dist.cpu().numpy().view(np.uint16)
+    nh, nhp = nh.cpu().numpy(), nhp.cpu().numpy()
+    ok = (d >= 0) & (d < V)
+    do, nho, nhpo = O.dest_tables(csr, d[ok], nthreads=NTHREADS)
+    np.testing.assert_array_equal(dist[ok], do)
+    np.testing.assert_array_equal(nh[ok], nho)
+    np.testing.assert_array_equal(nhp[ok], nhpo)
+    assert (dist[~ok] == 0xFFFF).all() and (nh[~ok] == -1).all()
 
 
 @pytest.mark.parametrize("name", G.MULTI)
