@@ -318,6 +318,7 @@ int sdnr_destroy(sdnr_ctx *ctx)
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->scratch2) (void)hipFree(ctx->scratch2);
     if (ctx->wq) (void)hipFree(ctx->wq);
+    if (ctx->dmat) (void)hipFree(ctx->dmat);
     if (ctx->stage) (void)hipFree(ctx->stage);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->h_flag) (void)hipHostFree(ctx->h_flag);

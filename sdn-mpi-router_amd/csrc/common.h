@@ -86,6 +86,8 @@ struct sdnr_ctx {
     size_t scratch2_bytes = 0;
     void *wq = nullptr;                 // source work queue of the split DFS (kFlagCuMap)
     size_t wq_bytes = 0;
+    void *dmat = nullptr;               // V x V distances behind APSP-derived shortest tables
+    size_t dmat_bytes = 0;
     bool port16 = false;                // every port fits the packed layout (< 0xFFFF)
     bool symmetric = false;             // every link (u, v) has its reverse (v, u)
 

@@ -1030,11 +1030,11 @@ static int launch_sp_apsp(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uin
                           int32_t *d_nh, int32_t *d_nh_port)
 {
     const int V = ctx->V;
-    // D lives in scratch2 (the APSP itself pads into scratch when V is not
-    // a multiple of its tile)
-    int rc = sdnr_reserve(&ctx->scratch2, &ctx->scratch2_bytes, (size_t)V * V * sizeof(uint16_t));
+    // D in its own buffer (the APSP keeps its pass flags in scratch2 and
+    // pads into scratch when V is not a multiple of its tile)
+    int rc = sdnr_reserve(&ctx->dmat, &ctx->dmat_bytes, (size_t)V * V * sizeof(uint16_t));
     if (rc) return rc;
-    uint16_t *D = static_cast<uint16_t *>(ctx->scratch2);
+    uint16_t *D = static_cast<uint16_t *>(ctx->dmat);
     const bool timed = ctx->timed;
     ctx->timed = false;                          // the caller's events bracket both parts
     rc = sdnr_launch_apsp(ctx, D);
