@@ -117,6 +117,91 @@ __global__ __launch_bounds__(256) void scan_add_kernel(int64_t *__restrict__ a, 
         a[i] += sums[i / kScanTile];
 }
 
+// Offsets in ONE pass (the default): lengths gathered from the hop table,
+// scanned per tile, and the tile prefixes chained by a decoupled look-back --
+// route_len + scan_tiles + scan_sums + scan_add made four passes over the
+// int64 offsets (k=48 all-pairs: 0.23 ms of every 16.7 M-pair chunk).  Tiles
+// are numbered by an arrival ticket, so a tile only ever waits for tiles that
+// already run; a tile's status word is flag << 62 | value (flag 1: the
+// tile's own total, 2: the inclusive prefix through it).  Wave 0 looks back
+// 64 tiles at a time.  Every spin is bounded (watchdog code kErrScan).
+constexpr uint64_t kStAgg = 1ull << 62, kStPre = 2ull << 62, kStVal = (1ull << 62) - 1;
+
+__global__ __launch_bounds__(kScanThreads) void route_offsets_fused_kernel(
+    int V, const int32_t *__restrict__ hops, const int32_t *__restrict__ rows,
+    const int32_t *__restrict__ dsts, int64_t n, int64_t *__restrict__ off,
+    uint64_t *__restrict__ st, int *__restrict__ err)
+{
+    __shared__ int64_t sh[kScanThreads];
+    __shared__ int64_t s_prefix;
+    __shared__ int64_t s_tile;
+    if (threadIdx.x == 0)
+        s_tile = (int64_t)atomicAdd(reinterpret_cast<unsigned long long *>(&st[0]), 1ull);
+    __syncthreads();
+    const int64_t tile = s_tile;
+    const int64_t base = tile * kScanTile + (int64_t)threadIdx.x * kScanItems;
+    int64_t v[kScanItems];
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const int64_t i = base + k;
+        int h = -1;
+        if (i < n) {
+            const int r = rows[i], d = dsts[i];
+            if (r >= 0 && d >= 0 && d < V) h = hops[(size_t)r * V + d];
+        }
+        v[k] = h < 0 ? 0 : (int64_t)h + 1;
+    }
+    const int64_t total = block_scan(v, sh);
+    uint64_t *status = st + 1;
+    if (threadIdx.x < SDNR_WAVE) {
+        const int lane = (int)threadIdx.x;
+        int64_t prefix = 0;
+        if (tile == 0) {
+            if (lane == 0)
+                __hip_atomic_store(&status[0], kStPre | (uint64_t)total, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0)
+                __hip_atomic_store(&status[tile], kStAgg | (uint64_t)total, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            int64_t j = tile - 1;
+            for (unsigned spin = 0;;) {
+                const int64_t idx = j - lane;
+                const uint64_t w = idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT)
+                                            : kStPre;               // before tile 0: prefix 0
+                const uint64_t mp = __ballot((w >> 62) == 2u);
+                const int fp = mp ? __ffsll((unsigned long long)mp) - 1 : SDNR_WAVE;
+                const uint64_t below = fp >= SDNR_WAVE ? ~0ull : ((2ull << fp) - 1ull);
+                if (__ballot((w >> 62) == 0u) & below) {            // a needed tile not published
+                    if (++spin > (1u << 22)) {
+                        if (lane == 0) atomicOr(err, kErrScan);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                int64_t x = lane <= fp ? (int64_t)(w & kStVal) : 0;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+                prefix += x;
+                if (fp < SDNR_WAVE) break;
+                j -= SDNR_WAVE;
+            }
+            if (lane == 0)
+                __hip_atomic_store(&status[tile], kStPre | (uint64_t)(prefix + total),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) s_prefix = prefix;
+    }
+    __syncthreads();
+    const int64_t prefix = s_prefix;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k)
+        if (base + k < n) off[base + k] = prefix + v[k];
+    if (threadIdx.x == 0 && (tile + 1) * kScanTile >= n) off[n] = prefix + total;
+}
+
 // anc_out[r][v] = a[r][b[r][v]] (-1 stays -1): composing the parent table
 // with itself by doubling gives the 2^j-th ancestor table of every tree
 __global__ __launch_bounds__(256) void tree_compose_kernel(int V, size_t n,
@@ -567,6 +652,16 @@ int sdnr_launch_route_offsets(sdnr_ctx *ctx, const int32_t *d_hops, const int32_
     const int64_t tiles = (n + kScanTile - 1) / kScanTile;
     int rc = sdnr_reserve(&ctx->scratch, &ctx->scratch_bytes, (size_t)(tiles + 1) * 8);
     if (rc) return rc;
+    // one pass (SDNROUTE_ROUTE_SCAN=4: the four-kernel form, A/B)
+    const char *sf = getenv("SDNROUTE_ROUTE_SCAN");
+    if (!(sf && !strcmp(sf, "4"))) {
+        uint64_t *st = static_cast<uint64_t *>(ctx->scratch);
+        SDNR_HIP(hipMemsetAsync(st, 0, (size_t)(tiles + 1) * 8, ctx->stream));
+        hipLaunchKernelGGL(route_offsets_fused_kernel, dim3((unsigned)tiles), dim3(kScanThreads), 0,
+                           ctx->stream, V, d_hops, d_rows, d_dsts, n, d_off, st, ctx->d_err);
+        SDNR_HIP(hipGetLastError());
+        return SDNR_OK;
+    }
     int64_t *sums = static_cast<int64_t *>(ctx->scratch);
     int g = (int)((n + 255) / 256);
     if (g > ctx->num_cus * 16) g = ctx->num_cus * 16;

@@ -908,3 +908,40 @@ def test_route_expand_packed_rejects_wide_last_port(ctx):
             with pytest.raises(_native.SdnrError) as ei:
                 ctx.synchronize()
             assert ei.value.code == -22 and "last port" in str(ei.value)
+
+
+@pytest.mark.parametrize("scan", ["fused", "4"])
+@pytest.mark.parametrize("npairs", [1, 8191, 8192, 8193, 3_000_000])
+def test_route_offsets_scan(ctx, monkeypatch, scan, npairs):
+    """sdnr_route_offsets: the one-pass look-back scan (default) and the
+    four-kernel form give offsets[i] = sum of (hops + 1) of the pairs before
+    i (0 for an unreachable pair or an unknown row / destination), on tile
+    boundaries and over hundreds of tiles (look-back windows past 64)."""
+    import torch
+    if scan == "4":
+        monkeypatch.setenv("SDNROUTE_ROUTE_SCAN", "4")
+    csr = T.fat_tree(8).csr()
+    ctx.upload(csr)
+    V = csr.V
+    srcs = np.arange(V, dtype=np.int32)
+    _, _, hop = O.dfs_tables(csr, srcs, nthreads=NTHREADS)
+    hop[3, 7] = -1                                # an unreachable pair
+    rng = np.random.default_rng(npairs)
+    rows = rng.integers(0, V, npairs).astype(np.int32)
+    dsts = rng.integers(0, V, npairs).astype(np.int32)
+    dsts[::97] = -1                               # unknown destinations
+    rows[5::101] = -1                             # unknown rows
+    lens = np.where((rows >= 0) & (dsts >= 0), 0, 0).astype(np.int64)
+    ok = (rows >= 0) & (dsts >= 0)
+    h = np.full(npairs, -1, np.int64)
+    h[ok] = hop[rows[ok], dsts[ok]]
+    lens = np.where(h < 0, 0, h + 1)
+    want = np.concatenate([[0], np.cumsum(lens)])
+    dev = torch.device("cuda", 0)
+    th = torch.from_numpy(hop).to(dev)
+    tr, td = torch.from_numpy(rows).to(dev), torch.from_numpy(dsts).to(dev)
+    off = torch.full((npairs + 1,), -7, dtype=torch.int64, device=dev)
+    ctx.route_offsets_device(th.data_ptr(), tr.data_ptr(), td.data_ptr(), npairs, off.data_ptr(),
+                             nrows=V)
+    ctx.synchronize()
+    np.testing.assert_array_equal(off.cpu().numpy(), want)
