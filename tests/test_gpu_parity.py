@@ -931,7 +931,6 @@ def test_route_offsets_scan(ctx, monkeypatch, scan, npairs):
     dsts = rng.integers(0, V, npairs).astype(np.int32)
     dsts[::97] = -1                               # unknown destinations
     rows[5::101] = -1                             # unknown rows
-    lens = np.where((rows >= 0) & (dsts >= 0), 0, 0).astype(np.int64)
     ok = (rows >= 0) & (dsts >= 0)
     h = np.full(npairs, -1, np.int64)
     h[ok] = hop[rows[ok], dsts[ok]]
