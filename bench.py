@@ -10,10 +10,14 @@ host-bearing edge switches = 27,648^2 = 7.64e8 host-pair routes.  Inputs
 (CSR, source list) are resident in HBM before the timed region; outputs stay
 in HBM.
 
-Multi-GPU (torchrun, one rank per GPU, RCCL): the sources are split into
-contiguous blocks, each rank builds its block, and one all-gather assembles
-the full [sources][V] tables on every rank (the exchange step of the north
-star); fixed total work -> "scaling": "strong".
+Multi-GPU (one rank per GPU, RCCL; ``--gpus N`` starts the N ranks itself
+when no launcher did): the sources are split into contiguous blocks, each
+rank builds its block, and the blocks are assembled over RCCL -- by default
+on rank 0, the controller's GPU (point-to-point receives, SURVEY.md 8(e)'s
+"or on GPU 0 only"), with ``--assemble all`` by an all-gather onto every
+rank; the other form is timed beside it.  Consecutive steps may be kept in
+flight on their own streams (``--inflight``) so that a rank's share fills
+its GPU.  Fixed total work per step -> "scaling": "strong".
 
 The JSON line also carries
   roofline      algorithmic bytes of the DFS kernel per launch
@@ -78,10 +82,16 @@ def parse():
                     help="dfs mode: skip the materialised flow-entry rate of every host pair")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0,
                     help="bound on the CPU baseline's work")
-    ap.add_argument("--assemble", choices=["all", "root"], default="all",
-                    help="N > 1: tables assembled on every rank (RCCL all-gather, default) "
-                         "or on rank 0 only (point-to-point receives into the root); the "
-                         "other form is measured beside it in the multi_gpu block")
+    ap.add_argument("--assemble", choices=["all", "root"], default="root",
+                    help="N > 1: tables assembled on rank 0, the controller's GPU (RCCL "
+                         "point-to-point receives into the root, default), or on every "
+                         "rank (RCCL all-gather); the other form is measured beside it in "
+                         "the multi_gpu block")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="N > 1: steps kept in flight on their own streams (0: auto -- as "
+                         "many as it takes for one rank's share of the sources to fill its "
+                         "GPU, at most 3; 1 at N = 1).  Every step still computes and "
+                         "assembles all tables")
     ap.add_argument("--rehearse", action="store_true",
                     help="launcher rehearsal on CPU: the N ranks form a gloo group, shard "
                          "the sources and assemble them, and rank 0 prints the line's "
@@ -901,9 +911,17 @@ def main():
                 torch.empty((per, V), dtype=torch.int32, device=dev),        # nh
                 torch.empty((per, V), dtype=torch.int32, device=dev))        # nh_port
 
-    # N > 1: two table sets, so step i+1's kernel (our stream) overlaps step
-    # i's all-gather (RCCL's stream); a set is reused only after its gather
-    nbuf = 2 if world > 1 else 1
+    # N > 1: one rank's share of the k=48 sources (144 at N = 8) fills an
+    # eighth of the GPU, and a source's search is a serial chain (DESIGN.md
+    # 4.1b): consecutive steps -- independent recomputations of the same
+    # tables -- run on their own streams so that a rank keeps about as many
+    # sources resident as one GPU holds at N = 1 (4 per CU); two table sets
+    # per stream, so a step's kernel overlaps the previous step's gather
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    inflight = args.inflight if args.inflight > 0 else \
+        (1 if world == 1 else max(1, min(3, -(-4 * cus // max(1, per)))))
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
+    nbuf = (2 if world > 1 else 1) * inflight
     bufs = [tables() for _ in range(nbuf)]
     gathered = [tuple(torch.empty((world * per, V), dtype=t.dtype, device=dev) for t in b)
                 for b in bufs]
@@ -913,33 +931,38 @@ def main():
 
     def step(ev=None):
         k = counter[0] % nbuf
+        st = streams[counter[0] % inflight]   # table set k always runs on stream k % inflight
         counter[0] += 1
-        for w in pending[k]:                # this set's previous gather is done
-            w.wait()
-        pending[k] = []
-        tb = bufs[k]
-        if ev is not None:
-            ev[0].record(stream)
-        if slots:
-            ctx.dfs_tables_slots_device(t_src.data_ptr(), per, tb[0].data_ptr())
-        elif packed:
-            ctx.dfs_tables_packed_device(t_src.data_ptr(), per, tb[0].data_ptr())
-        elif args.mode == "dfs":
-            ctx.dfs_tables_device(t_src.data_ptr(), per, tb[0].data_ptr(), tb[1].data_ptr())
-        else:
-            ctx.shortest_tables_device(t_src.data_ptr(), per, tb[0].data_ptr(), tb[1].data_ptr(),
-                                       tb[2].data_ptr())
-        if ev is not None:
-            ev[1].record(stream)
-        if world > 1:                       # assemble [sources][V] on every rank / rank 0
-            for t, g in zip(tb, gathered[k]):
-                pending[k].append(D.all_gather_rows_async(t, g) if assemble[0] == "all"
-                                  else D.gather_rows_to_root(t, g))
+        with torch.cuda.stream(st):
+            for w in pending[k]:            # this set's previous gather is done
+                w.wait()
+            pending[k] = []
+            tb = bufs[k]
+            if inflight > 1:
+                ctx.set_stream(st.cuda_stream)
+            if ev is not None:
+                ev[0].record(st)
+            if slots:
+                ctx.dfs_tables_slots_device(t_src.data_ptr(), per, tb[0].data_ptr())
+            elif packed:
+                ctx.dfs_tables_packed_device(t_src.data_ptr(), per, tb[0].data_ptr())
+            elif args.mode == "dfs":
+                ctx.dfs_tables_device(t_src.data_ptr(), per, tb[0].data_ptr(), tb[1].data_ptr())
+            else:
+                ctx.shortest_tables_device(t_src.data_ptr(), per, tb[0].data_ptr(),
+                                           tb[1].data_ptr(), tb[2].data_ptr())
+            if ev is not None:
+                ev[1].record(st)
+            if world > 1:                   # assemble [sources][V] on every rank / rank 0
+                for t, g in zip(tb, gathered[k]):
+                    pending[k].append(D.all_gather_rows_async(t, g) if assemble[0] == "all"
+                                      else D.gather_rows_to_root(t, g))
 
     def drain():
         for k in range(nbuf):
-            for w in pending[k]:
-                w.wait()
+            with torch.cuda.stream(streams[k % inflight]):
+                for w in pending[k]:
+                    w.wait()
             pending[k] = []
 
     for _ in range(args.warmup):
@@ -1014,8 +1037,11 @@ def main():
             "source_subset": bool(args.max_sources and S < (V if args.all_vertices
                                                              else len(np.unique(hv)))),
             "parallelism": "sources sharded over %d GPU(s)%s" % (
-                world, " + RCCL all-gather of the tables (double-buffered: step i+1's "
-                       "kernel overlaps step i's gather)" if world > 1 else ""),
+                world, (" + tables assembled %s over RCCL (double-buffered: step i+1's "
+                        "kernel overlaps step i's assembly)" % (
+                            "on every rank by all-gather" if args.assemble == "all"
+                            else "on rank 0 by point-to-point receives")) if world > 1 else ""),
+            "steps_in_flight": inflight,
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
