@@ -358,7 +358,8 @@ __global__ __launch_bounds__(256) void route_seg_packed_kernel(
     int V, const uint32_t *__restrict__ tree, Anc16 anc,
     const int32_t *__restrict__ rows, const int32_t *__restrict__ dsts,
     const int32_t *__restrict__ last_port, int npairs, const int64_t *__restrict__ off,
-    int32_t *__restrict__ hop_switch, int32_t *__restrict__ hop_port, int *__restrict__ err)
+    int32_t *__restrict__ hop_switch, int32_t *__restrict__ hop_port, int *__restrict__ err,
+    int diag)
 {
     __shared__ uint32_t seg_lds[4][CAP];
     __shared__ int lp_lds[4][64];
@@ -438,7 +439,8 @@ __global__ __launch_bounds__(256) void route_seg_packed_kernel(
                 continue;
             }
             // distinct paths of the n pairs, 4 at a time (16 lanes each)
-            uint64_t heads = __ballot(head && lane < n && pl > 0);
+            // diag 1 (timing diagnostic, SDNROUTE_ROUTE_DIAG): no route walks
+            uint64_t heads = (diag & 1) ? 0ull : __ballot(head && lane < n && pl > 0);
             while (heads) {
                 // the q-th lowest head for lane group q
                 const int q = lane >> 4, k = lane & 15;
@@ -470,7 +472,8 @@ __global__ __launch_bounds__(256) void route_seg_packed_kernel(
             // destination) pairs at a time: the run's entries are cnt copies
             // of one L-entry route, contiguous, so the lanes stream them with
             // full-wave stores (pair q, entry k of flat index t = q L + k)
-            uint64_t runs = __ballot(head && lane < n);
+            // diag 2 (timing diagnostic): no entry stores
+            uint64_t runs = (diag & 2) ? 0ull : __ballot(head && lane < n);
             while (runs) {
                 const int p0 = __builtin_ctzll(runs);
                 runs &= runs - 1;
@@ -721,34 +724,36 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
             const char *nt = getenv("SDNROUTE_ROUTE_NT");       // "1": non-temporal stores
             // 16-B stores of 4 entries per lane (SDNROUTE_ROUTE_V4=0: 4-B stores)
             const char *v4 = getenv("SDNROUTE_ROUTE_V4");
+            const char *dg = getenv("SDNROUTE_ROUTE_DIAG");   // timing only: 1 no walks, 2 no stores
+            const int diag = dg ? atoi(dg) : 0;
             if (d_entries) {
                 ctx->last_kernel = "route_seg_packed_kernel<1024,u32>";
                 if (v4 && !strcmp(v4, "0"))
                     hipLaunchKernelGGL((route_seg_packed_kernel<1024, false, true, false>),
                                        dim3((unsigned)g), dim3(256), 0, ctx->stream, ctx->V, tree,
                                        tabs, d_rows, d_dsts, d_last_port, npairs, d_off,
-                                       reinterpret_cast<int32_t *>(d_entries), nullptr, ctx->d_err);
+                                       reinterpret_cast<int32_t *>(d_entries), nullptr, ctx->d_err, diag);
                 else
                     hipLaunchKernelGGL((route_seg_packed_kernel<1024, false, true, true>),
                                        dim3((unsigned)g), dim3(256), 0, ctx->stream, ctx->V, tree,
                                        tabs, d_rows, d_dsts, d_last_port, npairs, d_off,
-                                       reinterpret_cast<int32_t *>(d_entries), nullptr, ctx->d_err);
+                                       reinterpret_cast<int32_t *>(d_entries), nullptr, ctx->d_err, diag);
             } else {
                 ctx->last_kernel = "route_seg_packed_kernel<1024>";
                 if (nt && !strcmp(nt, "1"))
                     hipLaunchKernelGGL((route_seg_packed_kernel<1024, true, false>), dim3((unsigned)g),
                                        dim3(256), 0, ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts,
-                                       d_last_port, npairs, d_off, d_switch, d_hport, nullptr);
+                                       d_last_port, npairs, d_off, d_switch, d_hport, nullptr, diag);
                 else if ((((uintptr_t)d_switch ^ (uintptr_t)d_hport) & 15u) == 0 && !(v4 && !strcmp(v4, "0")))
                     // both arrays share their 16-B phase: 16-B stores into each
                     hipLaunchKernelGGL((route_seg_packed_kernel<1024, false, false, true>),
                                        dim3((unsigned)g), dim3(256), 0, ctx->stream, ctx->V, tree,
                                        tabs, d_rows, d_dsts, d_last_port, npairs, d_off, d_switch,
-                                       d_hport, nullptr);
+                                       d_hport, nullptr, diag);
                 else
                     hipLaunchKernelGGL((route_seg_packed_kernel<1024, false, false>), dim3((unsigned)g),
                                        dim3(256), 0, ctx->stream, ctx->V, tree, tabs, d_rows, d_dsts,
-                                       d_last_port, npairs, d_off, d_switch, d_hport, nullptr);
+                                       d_last_port, npairs, d_off, d_switch, d_hport, nullptr, diag);
             }
         } else {
             int64_t g = ((int64_t)npairs * 16 + 255) / 256;
