@@ -129,6 +129,7 @@ inline void sdnr_allow_lds(const void *fn, size_t bytes)
 constexpr int kErrLastPort = 256;   // sdnr_route_expand_packed: a last port outside [0, 0xFFFF]
 constexpr int kErrTreeClimb = 512;  // sdnr_dfs_rows_affected: a tree climb outran V steps
 constexpr int kErrScan = 1024;      // sdnr_route_offsets: a look-back wait ran out
+constexpr int kErrSeg = 2048;       // route expansion: a walker / storer hand-off wait ran out
 
 // error plumbing (capi.hip)
 int sdnr_fail(int code, const char *fmt, ...);

@@ -22,6 +22,7 @@
 // popcount(k) loads; route_walk_kernel (one lane per pair,
 // SDNROUTE_ROUTE_WALK=serial) is the plain form.  The tree rows stay L2 / Infinity-Cache resident; the output is
 // written once.
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -594,6 +595,290 @@ __global__ __launch_bounds__(256) void route_seg_packed_kernel(
     }
 }
 
+// Walkers and storers (the default u32 / int32 expansion on packed trees).
+// A GCN / CDNA wave's vector-memory counter retires loads AND stores in
+// issue order, so in route_seg_packed_kernel every load of the next group
+// (its pairs, then each step of a route walk) first waited for the previous
+// group's entry stores to be acknowledged -- at the all-pairs write rate,
+// microseconds per group (diagnostic: walks alone 9 ms, stores alone 51 ms,
+// both 73 ms on k=48).  Here the roles are separate waves of one workgroup:
+// NWK walker waves take the 64-pair groups (pairs, distinct routes walked
+// into an LDS slot, run descriptors) and never store; NST storer waves take
+// full slots and only read LDS and store, so neither kind of wave ever waits
+// on the other's memory traffic.  Walker w owns NSL slots (a ring with
+// produced / consumed counters in LDS); storer j serves walkers j, j + NST,
+// ...  A pair whose route outgrows a slot is walked straight to global
+// memory by its walker, as before.  Bounded spins (watchdog kErrSeg).
+template <int CAP>
+struct SegSlot {
+    uint32_t buf[CAP];            // the distinct routes' entries
+    int lps[64];                  // last (host) port per pair
+    int dlo[64], dhi[64];         // run descriptors by head lane: output offset,
+    int dso[64], dL[64], dd[64];  //   route offset in buf, entries per pair, destination
+    uint32_t mlo, mhi;            // run heads (lane mask)
+    int n;                        // pairs in the slot
+};
+
+template <int CAP, bool OUTP, int NWK, int NST, int NSL>
+__global__ __launch_bounds__((NWK + NST) * 64) void route_seg_pipe_kernel(
+    int V, const uint32_t *__restrict__ tree, Anc16 anc,
+    const int32_t *__restrict__ rows, const int32_t *__restrict__ dsts,
+    const int32_t *__restrict__ last_port, int npairs, const int64_t *__restrict__ off,
+    int32_t *__restrict__ hop_switch, int32_t *__restrict__ hop_port, int *__restrict__ err)
+{
+    static_assert(NWK % NST == 0, "each storer serves NWK / NST walkers");
+    constexpr unsigned kSpin = 1u << 24;
+    __shared__ SegSlot<CAP> slots[NWK * NSL];
+    __shared__ int prod[NWK], cons[NWK], done[NWK];
+    const int lane = lane_id();
+    const int w = uniform((int)(threadIdx.x >> 6));
+    if (threadIdx.x < NWK) {
+        prod[threadIdx.x] = 0;
+        cons[threadIdx.x] = 0;
+        done[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    const int groups = (npairs + 63) >> 6;
+    const uint16_t *__restrict__ anc16 = anc.a[4];
+    if (w < NWK) {
+        // ------------------------------------------------------ a walker
+        int P = 0;
+        for (int g = blockIdx.x * NWK + w; g < groups; g += gridDim.x * NWK) {
+            const int gend = min(npairs, (g + 1) * 64);
+            for (int base = g * 64; base < gend;) {
+                const int i = base + lane;
+                const bool valid = i < gend;
+                int r = -1, d = -1, lp = 0;
+                int64_t lo = 0;
+                int L = 0;
+                if (valid) {
+                    r = rows[i];
+                    d = dsts[i];
+                    lp = last_port[i];
+                    lo = off[i];
+                    L = (int)(off[i + 1] - lo);
+                }
+                if (OUTP && __ballot(L > 0 && (uint32_t)lp > 0xFFFFu) && lane == 0)
+                    atomicOr(err, kErrLastPort);
+                const int pl = L > 0 ? L - 1 : 0;
+                const int pr = __shfl_up(r, 1, 64), pd = __shfl_up(d, 1, 64);
+                const bool head = valid && (lane == 0 || pr != r || pd != d);
+                const int c = head ? pl : 0;
+                const int incl = wave_incl_scan(c);
+                const int segoff = head ? incl - c : incl - pl;
+                const uint64_t fit = __ballot(valid && incl <= CAP);
+                const int n = fit == ~0ull ? 64 : __builtin_ctzll(~fit);
+                if (n == 0) {
+                    // one pair longer than a slot: walked straight to global
+                    // memory here (these stores are the walker's own)
+                    const int64_t lo0 = (int64_t)(uint32_t)read_lane((int)lo, 0) |
+                                        ((int64_t)read_lane((int)(lo >> 32), 0) << 32);
+                    const int h = read_lane(pl, 0);
+                    const size_t rb = (size_t)read_lane(r, 0) * V;
+                    if (lane < 16) {
+                        const int k = lane;
+                        int y = read_lane(d, 0);
+                        uint32_t *ent = reinterpret_cast<uint32_t *>(hop_switch);
+                        if (k == 0) {
+                            if (OUTP) {
+                                ent[lo0 + h] = (uint32_t)y | ((uint32_t)read_lane(lp, 0) << 16);
+                            } else {
+                                hop_switch[lo0 + h] = y;
+                                hop_port[lo0 + h] = read_lane(lp, 0);
+                            }
+                        }
+                        if (k < h) {
+                            if (k & 1) y = (int)(tree[rb + y] & 0xFFFFu);
+#pragma unroll
+                            for (int j = 1; j < 4; ++j)
+                                if (k & (1 << j)) y = anc.a[j][rb + y];
+                            for (int u = k; u < h; u += 16) {
+                                const uint32_t e = tree[rb + y];
+                                if (OUTP) {
+                                    ent[lo0 + h - u - 1] = e;
+                                } else {
+                                    hop_switch[lo0 + h - u - 1] = (int32_t)(e & 0xFFFFu);
+                                    hop_port[lo0 + h - u - 1] = (int32_t)(e >> 16);
+                                }
+                                if (u + 16 < h) y = anc16[rb + y];
+                            }
+                        }
+                    }
+                    base += 1;
+                    continue;
+                }
+                // a free slot of this walker's ring
+                for (unsigned spin = 0;
+                     P - __hip_atomic_load(&cons[w], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= NSL;
+                     ++spin) {
+                    if (spin > kSpin) {
+                        if (lane == 0) atomicOr(err, kErrSeg);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                SegSlot<CAP> &sl = slots[w * NSL + P % NSL];
+                // distinct paths of the n pairs, 4 at a time (16 lanes each)
+                uint64_t heads = __ballot(head && lane < n && pl > 0);
+                while (heads) {
+                    const int q = lane >> 4, k = lane & 15;
+                    uint64_t hm = heads;
+                    for (int t = 0; t < q && hm; ++t) hm &= hm - 1;
+                    const int hl = hm ? __builtin_ctzll(hm) : -1;
+                    const int src_lane = hl < 0 ? 0 : hl;
+                    const int hr = __shfl(r, src_lane, 64), hd = __shfl(d, src_lane, 64);
+                    const int h = __shfl(pl, src_lane, 64), so = __shfl(segoff, src_lane, 64);
+                    if (hl >= 0 && k < h) {
+                        const size_t rb = (size_t)hr * V;
+                        int y = hd;
+                        if (k & 1) y = (int)(tree[rb + y] & 0xFFFFu);
+#pragma unroll
+                        for (int j = 1; j < 4; ++j)
+                            if (k & (1 << j)) y = anc.a[j][rb + y];
+                        for (int u = k; u < h; u += 16) {
+                            sl.buf[so + h - u - 1] = tree[rb + y];
+                            if (u + 16 < h) y = anc16[rb + y];
+                        }
+                    }
+                    for (int t = 0; t < 4 && heads; ++t) heads &= heads - 1;
+                }
+                sl.lps[lane] = lp;
+                const uint64_t runs = __ballot(head && lane < n);
+                if (head && lane < n) {
+                    sl.dlo[lane] = (int)(uint32_t)lo;
+                    sl.dhi[lane] = (int)(lo >> 32);
+                    sl.dso[lane] = segoff;
+                    sl.dL[lane] = L;
+                    sl.dd[lane] = d;
+                }
+                if (lane == 0) {
+                    sl.mlo = (uint32_t)runs;
+                    sl.mhi = (uint32_t)(runs >> 32);
+                    sl.n = n;
+                }
+                ++P;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                if (lane == 0) __hip_atomic_store(&prod[w], P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                base += n;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        if (lane == 0) __hip_atomic_store(&done[w], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return;
+    }
+    // ---------------------------------------------------------- a storer
+    constexpr int PER = NWK / NST;                // walkers served
+    const int js = w - NWK;
+    int C[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) C[q] = 0;
+    for (unsigned spin = 0;;) {
+        bool progress = false, finished = true;
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int ww = js + q * NST;
+            const int dn = __hip_atomic_load(&done[ww], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int Pw = __hip_atomic_load(&prod[ww], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (C[q] >= Pw) {
+                finished = finished && dn;
+                continue;
+            }
+            finished = false;
+            progress = true;
+            const SegSlot<CAP> &sl = slots[ww * NSL + C[q] % NSL];
+            const int n = sl.n;
+            uint64_t runs = (uint64_t)sl.mlo | ((uint64_t)sl.mhi << 32);
+            while (runs) {
+                const int p0 = __builtin_ctzll(runs);
+                runs &= runs - 1;
+                const int p1 = runs ? __builtin_ctzll(runs) : n;
+                const int Lr = sl.dL[p0];
+                if (Lr <= 0) continue;
+                const int64_t lop = (int64_t)(uint32_t)sl.dlo[p0] | ((int64_t)sl.dhi[p0] << 32);
+                const int sop = sl.dso[p0], dp = sl.dd[p0];
+                const int total = (p1 - p0) * Lr;
+                const float inv = 1.0f / (float)Lr;
+                auto qk = [&](int t, int &q2, int &k) {
+                    q2 = (int)((float)t * inv);
+                    k = t - q2 * Lr;
+                    if (k >= Lr) { ++q2; k -= Lr; }
+                    if (k < 0) { --q2; k += Lr; }
+                };
+                auto sw_of = [&](int k) -> uint32_t {
+                    return k < Lr - 1 ? (sl.buf[sop + k] & 0xFFFFu) : (uint32_t)dp;
+                };
+                auto pt_of = [&](int q2, int k) -> uint32_t {
+                    return k < Lr - 1 ? (sl.buf[sop + k] >> 16) : (uint32_t)sl.lps[p0 + q2];
+                };
+                auto word = [&](int q2, int k) -> uint32_t {
+                    return k < Lr - 1 ? sl.buf[sop + k] : (uint32_t)dp | ((uint32_t)sl.lps[p0 + q2] << 16);
+                };
+                uint32_t *o = reinterpret_cast<uint32_t *>(hop_switch) + lop;
+                uint32_t *op = OUTP ? nullptr : reinterpret_cast<uint32_t *>(hop_port) + lop;
+                auto put1 = [&](int t) {
+                    int q2, k;
+                    qk(t, q2, k);
+                    if (OUTP) {
+                        o[t] = word(q2, k);
+                    } else {
+                        o[t] = sw_of(k);
+                        op[t] = pt_of(q2, k);
+                    }
+                };
+                // 16-B stores of 4 entries per lane when the run fills a
+                // pass and both arrays share the 16-B phase (int32 form)
+                const bool v4 = total >= 256 &&
+                                (OUTP || ((((uintptr_t)o ^ (uintptr_t)op) & 15u) == 0));
+                if (v4) {
+                    const int hd = min(total, (int)(((16u - ((uint32_t)(uintptr_t)o & 15u)) & 15u) >> 2));
+                    if (lane < hd) put1(lane);
+                    const int bend = hd + ((total - hd) & ~3);
+                    for (int t0 = hd; t0 < bend; t0 += 256) {
+                        const int t = t0 + 4 * lane;
+                        if (t < bend) {
+                            int q2, k;
+                            qk(t, q2, k);
+                            uint32_t a[4], b[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                if (OUTP) {
+                                    a[u] = word(q2, k);
+                                } else {
+                                    a[u] = sw_of(k);
+                                    b[u] = pt_of(q2, k);
+                                }
+                                if (++k == Lr) { k = 0; ++q2; }
+                            }
+                            *reinterpret_cast<uint4 *>(o + t) = make_uint4(a[0], a[1], a[2], a[3]);
+                            if (!OUTP)
+                                *reinterpret_cast<uint4 *>(op + t) = make_uint4(b[0], b[1], b[2], b[3]);
+                        }
+                    }
+                    if (bend + lane < total) put1(bend + lane);
+                } else {
+                    for (int t0 = 0; t0 < total; t0 += 64)
+                        if (t0 + lane < total) put1(t0 + lane);
+                }
+            }
+            ++C[q];
+            // the slot's LDS reads are done (their values are in the store
+            // registers): hand it back
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            if (lane == 0) __hip_atomic_store(&cons[ww], C[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (finished) break;
+        if (progress) {
+            spin = 0;
+        } else {
+            if (++spin > kSpin) {
+                if (lane == 0) atomicOr(err, kErrSeg);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void route_walk_kernel(
     int V, const int32_t *__restrict__ parent, const int32_t *__restrict__ port,
     const int32_t *__restrict__ rows, const int32_t *__restrict__ dsts,
@@ -726,6 +1011,50 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
             const char *v4 = getenv("SDNROUTE_ROUTE_V4");
             const char *dg = getenv("SDNROUTE_ROUTE_DIAG");   // timing only: 1 no walks, 2 no stores
             const int diag = dg ? atoi(dg) : 0;
+            // walker / storer waves (route_seg_pipe_kernel): SDNROUTE_ROUTE_PIPE=0
+            // keeps the one-role kernel, "W,S,N" picks walkers, storers and
+            // slots per walker among the compiled shapes
+            int pw = 4, ps = 2, pn = 2;
+            bool pipe = !(v4 && !strcmp(v4, "0")) && !(nt && !strcmp(nt, "1")) && !diag;
+            if (const char *pp = getenv("SDNROUTE_ROUTE_PIPE")) {
+                if (!strcmp(pp, "0")) pipe = false;
+                else if (sscanf(pp, "%d,%d,%d", &pw, &ps, &pn) != 3) pw = 4, ps = 2, pn = 2;
+            }
+            if (pipe) {
+                bool launched = false;
+#define SDNR_PIPE(W_, S_, N_)                                                                 \
+    if (!launched && pw == W_ && ps == S_ && pn == N_) {                                     \
+        constexpr size_t kL = sizeof(SegSlot<512>) * W_ * N_;                                \
+        size_t per_cu = SDNR_LDS_PER_CU / (kL + 256);                                        \
+        if (per_cu > (size_t)(32 / (W_ + S_))) per_cu = 32 / (W_ + S_);                       \
+        if (per_cu < 1) per_cu = 1;                                                          \
+        int64_t pg = (((int64_t)npairs + 63) / 64 + W_ - 1) / W_;                            \
+        if (pg > (int64_t)ctx->num_cus * (int64_t)per_cu) pg = (int64_t)ctx->num_cus * per_cu; \
+        if (d_entries)                                                                       \
+            hipLaunchKernelGGL((route_seg_pipe_kernel<512, true, W_, S_, N_>), dim3((unsigned)pg), \
+                               dim3((W_ + S_) * 64), 0, ctx->stream, ctx->V, tree, tabs, d_rows, \
+                               d_dsts, d_last_port, npairs, d_off,                           \
+                               reinterpret_cast<int32_t *>(d_entries), nullptr, ctx->d_err);  \
+        else                                                                                 \
+            hipLaunchKernelGGL((route_seg_pipe_kernel<512, false, W_, S_, N_>), dim3((unsigned)pg), \
+                               dim3((W_ + S_) * 64), 0, ctx->stream, ctx->V, tree, tabs, d_rows, \
+                               d_dsts, d_last_port, npairs, d_off, d_switch, d_hport, ctx->d_err); \
+        launched = true;                                                                     \
+    }
+                SDNR_PIPE(4, 2, 2)
+                SDNR_PIPE(4, 4, 2)
+                SDNR_PIPE(6, 2, 2)
+                SDNR_PIPE(4, 2, 3)
+                SDNR_PIPE(2, 2, 3)
+                SDNR_PIPE(8, 4, 2)
+                SDNR_PIPE(6, 3, 2)
+#undef SDNR_PIPE
+                if (!launched) return sdnr_fail(SDNR_ERR_INVAL, "SDNROUTE_ROUTE_PIPE=%d,%d,%d: no such shape", pw, ps, pn);
+                ctx->last_kernel = d_entries ? "route_seg_pipe_kernel<u32>" : "route_seg_pipe_kernel<int32>";
+                SDNR_HIP(hipGetLastError());
+                if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev1, ctx->stream));
+                return SDNR_OK;
+            }
             if (d_entries) {
                 ctx->last_kernel = "route_seg_packed_kernel<1024,u32>";
                 if (v4 && !strcmp(v4, "0"))
