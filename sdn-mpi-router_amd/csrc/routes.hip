@@ -1016,11 +1016,13 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
             // walker / storer waves (route_seg_pipe_kernel): SDNROUTE_ROUTE_PIPE=0
             // keeps the one-role kernel, "W,S,N" picks walkers, storers and
             // slots per walker among the compiled shapes
-            int pw = 4, ps = 2, pn = 2;
+            // k=48 all-pairs, same box: 2,2,3 69.5 ms; one-role 73.7; 4,4,2
+            // 73.6; 8,4,2 72.2; 4,2,2 92.3; 6,2,2 91.5; 6,3,2 107.6; 4,2,3 144.7
+            int pw = 2, ps = 2, pn = 3;
             bool pipe = !(v4 && !strcmp(v4, "0")) && !(nt && !strcmp(nt, "1")) && !diag;
             if (const char *pp = getenv("SDNROUTE_ROUTE_PIPE")) {
                 if (!strcmp(pp, "0")) pipe = false;
-                else if (sscanf(pp, "%d,%d,%d", &pw, &ps, &pn) != 3) pw = 4, ps = 2, pn = 2;
+                else if (sscanf(pp, "%d,%d,%d", &pw, &ps, &pn) != 3) pw = 2, ps = 2, pn = 3;
             }
             if (pipe) {
                 bool launched = false;
@@ -1050,6 +1052,11 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
                 SDNR_PIPE(2, 2, 3)
                 SDNR_PIPE(8, 4, 2)
                 SDNR_PIPE(6, 3, 2)
+                SDNR_PIPE(2, 2, 2)
+                SDNR_PIPE(2, 2, 4)
+                SDNR_PIPE(1, 1, 4)
+                SDNR_PIPE(3, 3, 2)
+                SDNR_PIPE(2, 1, 3)
 #undef SDNR_PIPE
                 if (!launched) return sdnr_fail(SDNR_ERR_INVAL, "SDNROUTE_ROUTE_PIPE=%d,%d,%d: no such shape", pw, ps, pn);
                 ctx->last_kernel = d_entries ? "route_seg_pipe_kernel<u32>" : "route_seg_pipe_kernel<int32>";

@@ -425,7 +425,8 @@ def test_route_entries_runs_and_long_paths(monkeypatch, fab):
     for a, b in ((o1, o2), (d1, d2), (p1, p2)):
         np.testing.assert_array_equal(a, b)
     # walker / storer shapes, and the one-role kernel, both forms
-    for shape in ("0", "4,4,2", "6,2,2", "4,2,3", "2,2,3", "8,4,2", "6,3,2"):
+    for shape in ("0", "4,4,2", "6,2,2", "4,2,3", "4,2,2", "8,4,2", "6,3,2", "2,2,2", "2,2,4",
+                  "1,1,4", "3,3,2", "2,1,3"):
         monkeypatch.setenv("SDNROUTE_ROUTE_PIPE", shape)
         for out in ("int32", "u32"):
             monkeypatch.setenv("SDNROUTE_ROUTE_OUT", out)
