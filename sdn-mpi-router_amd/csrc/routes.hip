@@ -1016,13 +1016,19 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
             // walker / storer waves (route_seg_pipe_kernel): SDNROUTE_ROUTE_PIPE=0
             // keeps the one-role kernel, "W,S,N" picks walkers, storers and
             // slots per walker among the compiled shapes
-            // k=48 all-pairs, same box: 2,2,3 69.5 ms; one-role 73.7; 4,4,2
-            // 73.6; 8,4,2 72.2; 4,2,2 92.3; 6,2,2 91.5; 6,3,2 107.6; 4,2,3 144.7
-            int pw = 2, ps = 2, pn = 3;
-            bool pipe = !(v4 && !strcmp(v4, "0")) && !(nt && !strcmp(nt, "1")) && !diag;
+            // k=48 all-pairs u32 entries, same box (gpurun_out/r5_f, r5_h): 2,2,4
+            // 69.1-69.3 ms, 2,2,3 69.1-69.5; one-role 73.6-73.9; 4,4,2 73.3-73.6;
+            // 8,4,2 72.2; 2,2,2 78.8; 3,3,2 79.6; 2,1,3 79.8; 4,2,2 92.3;
+            // 1,1,4 91.8; 6,2,2 91.5; 6,3,2 107.6; 4,2,3 144.7.  The int32 form
+            // gains nothing (116.4 one-role, 115.6 at 2,2,4) and short runs of
+            // random rank pairs lose (1,024-rank flows 0.50 -> 0.61 ms), so the
+            // pipeline serves large u32 batches only
+            int pw = 2, ps = 2, pn = 4;
+            bool pipe = d_entries && npairs >= (1 << 22) && !(v4 && !strcmp(v4, "0")) &&
+                        !(nt && !strcmp(nt, "1")) && !diag;
             if (const char *pp = getenv("SDNROUTE_ROUTE_PIPE")) {
                 if (!strcmp(pp, "0")) pipe = false;
-                else if (sscanf(pp, "%d,%d,%d", &pw, &ps, &pn) != 3) pw = 2, ps = 2, pn = 3;
+                else if (sscanf(pp, "%d,%d,%d", &pw, &ps, &pn) == 3) pipe = !diag;
             }
             if (pipe) {
                 bool launched = false;

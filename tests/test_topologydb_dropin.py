@@ -321,16 +321,16 @@ def test_route_entries_batched_fake_engine():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("walk", ["auto", "seg32", "v1", "v1seg32", "jump16", "serial", "int32",
-                                  "p4", "p8", "pipe0", "pipe0seg32"])
+                                  "p4", "p8", "pipe224", "pipe224seg32"])
 @pytest.mark.parametrize("name", ["mock", "fat_tree_k8", "dragonfly_a4_h2_p2", "random_V40",
                                   "torus_5x3x2"])
 def test_route_entries_match_reference(monkeypatch, name, walk):
     """GPU flow-entry emission for every host pair (plus switch-local and
     unknown MACs) equals the reference's fdb lists."""
     from oracle import oracle as O
-    if walk.startswith("pipe0"):                 # one-role waves (route_seg_packed_kernel)
-        monkeypatch.setenv("SDNROUTE_ROUTE_PIPE", "0")
-        if walk == "pipe0seg32":
+    if walk.startswith("pipe224"):               # walker / storer waves (route_seg_pipe_kernel)
+        monkeypatch.setenv("SDNROUTE_ROUTE_PIPE", "2,2,4")
+        if walk == "pipe224seg32":
             monkeypatch.setenv("SDNROUTE_ROUTE_OUT", "int32")
     elif walk == "serial":
         monkeypatch.setenv("SDNROUTE_ROUTE_WALK", walk)
@@ -375,13 +375,13 @@ def test_route_entries_k48_many_pairs(monkeypatch):
     assert db.engine.ctx.last_kernel() == "route_walk_kernel"
     monkeypatch.delenv("SDNROUTE_ROUTE_WALK")
     o1, d1, p1 = db.route_entries(pairs)
-    assert db.engine.ctx.last_kernel() == "route_seg_pipe_kernel<u32>"
+    assert db.engine.ctx.last_kernel() == "route_seg_packed_kernel<1024,u32>"
     np.testing.assert_array_equal(o0, o1)
     np.testing.assert_array_equal(d0, d1)
     np.testing.assert_array_equal(p0, p1)
     monkeypatch.setenv("SDNROUTE_ROUTE_OUT", "int32")
     o3, d3, p3 = db.route_entries(pairs)
-    assert db.engine.ctx.last_kernel() == "route_seg_pipe_kernel<int32>"
+    assert db.engine.ctx.last_kernel() == "route_seg_packed_kernel<1024>"
     np.testing.assert_array_equal(o0, o3)
     np.testing.assert_array_equal(d0, d3)
     np.testing.assert_array_equal(p0, p3)
@@ -418,10 +418,10 @@ def test_route_entries_runs_and_long_paths(monkeypatch, fab):
     o0, d0, p0 = db.route_entries(pairs)
     monkeypatch.delenv("SDNROUTE_ROUTE_WALK")
     o1, d1, p1 = db.route_entries(pairs)
-    assert db.engine.ctx.last_kernel() == "route_seg_pipe_kernel<u32>"
+    assert db.engine.ctx.last_kernel() == "route_seg_packed_kernel<1024,u32>"
     monkeypatch.setenv("SDNROUTE_ROUTE_OUT", "int32")
     o2, d2, p2 = db.route_entries(pairs)
-    assert db.engine.ctx.last_kernel() == "route_seg_pipe_kernel<int32>"
+    assert db.engine.ctx.last_kernel() == "route_seg_packed_kernel<1024>"
     for a, b in ((o1, o2), (d1, d2), (p1, p2)):
         np.testing.assert_array_equal(a, b)
     # walker / storer shapes, and the one-role kernel, both forms
@@ -736,7 +736,7 @@ def test_route_entries_wide_host_port(monkeypatch):
     pairs = [(a, b) for a in macs for b in macs]
     want = [O.find_route_pair(db, a, b) for a, b in pairs]
     assert db.find_routes(pairs) == want
-    assert db.engine.ctx.last_kernel() == "route_seg_pipe_kernel<int32>"   # int32 form
+    assert db.engine.ctx.last_kernel() == "route_seg_packed_kernel<1024>"   # int32 form
     narrow = [(a, b) for a, b in pairs if b != wide]
     assert db.find_routes(narrow) == [O.find_route_pair(db, a, b) for a, b in narrow]
-    assert db.engine.ctx.last_kernel() == "route_seg_pipe_kernel<u32>"
+    assert db.engine.ctx.last_kernel() == "route_seg_packed_kernel<1024,u32>"
