@@ -46,7 +46,10 @@ __global__ __launch_bounds__(256) void route_len_kernel(
     }
 }
 
-// block-wide exclusive scan of kScanTile values in place; block total out
+// block-wide exclusive scan of kScanTile values in place; block total out.
+// Each thread's kScanItems serially, the thread totals by a wave scan (six
+// shuffles), the 16 wave totals through LDS -- two barriers per tile (a
+// Hillis-Steele pass over the 1,024 thread totals took twenty).
 __device__ int64_t block_scan(int64_t (&v)[kScanItems], int64_t *sh)
 {
     int64_t t = 0;
@@ -56,20 +59,32 @@ __device__ int64_t block_scan(int64_t (&v)[kScanItems], int64_t *sh)
         v[k] = t;
         t += x;
     }
-    // inclusive scan of the per-thread totals across the block
-    sh[threadIdx.x] = t;
-    __syncthreads();
-    for (int o = 1; o < kScanThreads; o <<= 1) {
-        const int64_t y = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0;
-        __syncthreads();
-        sh[threadIdx.x] += y;
-        __syncthreads();
+    const int lane = lane_id(), wv = (int)(threadIdx.x >> 6);
+    int64_t incl = t;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
     }
-    const int64_t excl = sh[threadIdx.x] - t;
-    const int64_t total = sh[kScanThreads - 1];
+    constexpr int kWaves = kScanThreads / 64;
+    if (lane == 63) sh[wv] = incl;                 // wave totals
     __syncthreads();
+    if (wv == 0) {
+        int64_t w = lane < kWaves ? sh[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < kWaves; o <<= 1) {
+            const int64_t y = __shfl_up(w, o, 64);
+            if (lane >= o) w += y;
+        }
+        if (lane < kWaves) sh[kWaves + lane] = w;   // inclusive wave prefixes
+    }
+    __syncthreads();
+    const int64_t wave_excl = wv == 0 ? 0 : sh[kWaves + wv - 1];
+    const int64_t total = sh[2 * kWaves - 1];
+    const int64_t excl = wave_excl + incl - t;
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k) v[k] += excl;
+    __syncthreads();                               // sh reusable by the caller
     return total;
 }
 
