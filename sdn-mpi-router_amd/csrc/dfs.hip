@@ -1066,6 +1066,10 @@ constexpr int kFlagHops16 = 32;
 // split kernel: sources taken from the CU's own contiguous chunk (see
 // split_next_source) instead of the static blockIdx-strided order
 constexpr int kFlagCuMap = 64;
+// async kernel: when every fresh child of a candidate is a leaf, the next
+// candidate comes off the stack -- read its window, counts and row before
+// the push instead of after it
+constexpr int kFlagSpecPop = 128;
 
 // s_getreg encodings: (size - 1) << 11 | offset << 6 | register id
 constexpr int kHwIdReg = (31 << 11) | 4;      // HW_REG_HW_ID: cu [11:8], sh [12], se [14:13]
@@ -1811,6 +1815,36 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                     below = __popcll(mm & ((1ull << hl) - 1ull));   // fresh children under it
                     pu[0] = nu;
                     xp[0] = adj[(size_t)nu * 64 + lane];
+                } else if ((flags & kFlagSpecPop) && sp > 0) {
+                    // every fresh child is a leaf (its count is 0 and counts
+                    // never rise), so none stays on the stack and the next
+                    // candidate is the first entry with a count from the top
+                    // of the stack as it is NOW: the push below writes only
+                    // above sp and changes no count.  Its window, counts and
+                    // row are read here, so the row load runs beside the
+                    // push (a count read early is at most staler -- high --
+                    // which the row check absorbs).  A window without a
+                    // candidate is skipped as the outer loop would.
+                    const int kk = sp < 64 ? sp : 64;
+                    const int at = sp - 1 - lane;
+                    int e2 = stk[at < 0 ? 0 : at];
+                    e2 = lane < kk ? e2 : V;
+                    uint32_t c2;
+                    if constexpr (C16)
+                        c2 = (cnt[swz(e2 >> 1)] >> ((e2 & 1) << 4)) & 0xFFFFu;
+                    else
+                        c2 = cnt[swz(e2)];
+                    const uint64_t m2 = __ballot(c2 != 0u);
+                    if (m2) {
+                        const int f2 = __ffsll((unsigned long long)m2) - 1;
+                        nu = read_lane(e2, f2);
+                        sp -= f2 + 1;
+                        pu[0] = nu;
+                        xp[0] = adj[(size_t)nu * 64 + lane];
+                    } else {
+                        sp -= kk;
+                        pu[0] = -1;
+                    }
                 } else {
                     pu[0] = -1;                  // the next candidate comes off the stack
                 }
@@ -2656,7 +2690,11 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         const char *pz = getenv("SDNROUTE_DFS_PRESWZ");
         const uint16_t *rw = c16 ? ctx->radjc : ctx->radjw;
         const bool preswz = rw && !(pz && !strcmp(pz, "0"));
-        const int aflags = dfs_flags(kFlagPrio) | (preswz ? kFlagPreSwz : 0) | hflags;
+        // speculative stack pops (SDNROUTE_DFS_SPECPOP=0|1)
+        bool specpop = false;
+        if (const char *f = getenv("SDNROUTE_DFS_SPECPOP")) specpop = !strcmp(f, "1");
+        const int aflags = dfs_flags(kFlagPrio) | (preswz ? kFlagPreSwz : 0) | hflags |
+                           (specpop ? kFlagSpecPop : 0);
         // paired worker rows (in-degree <= 32, pre-swizzled rows only);
         // else, at <= 2 sources per CU (the 5-worker regime), dword-paired
         // rows: k=48 1 / 144 sources 56.3 / 57.8 -> 54.7 / 56.4 us; at the

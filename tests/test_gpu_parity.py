@@ -211,15 +211,37 @@ def test_dfs_packed_k48_worker_count(ctx, monkeypatch, nsrc):
     np.testing.assert_array_equal(tree, _pack(po, to))
 
 
+@pytest.mark.parametrize("spec", ["0", "1"])
+@pytest.mark.parametrize("nsrc", [1, 144, 1152])
+@pytest.mark.parametrize("name", ["fat_tree_k48", "dragonfly_a16_h8_p8"])
+def test_dfs_async_speculative_pop(ctx, monkeypatch, name, nsrc, spec):
+    """The async kernel with the next stack candidate (window, counts, row)
+    read before the push whenever every fresh child is a leaf
+    (SDNROUTE_DFS_SPECPOP), and without: packed trees bit-exact vs the
+    oracle at 1, 144 and 1,152 sources (every worker regime)."""
+    monkeypatch.setenv("SDNROUTE_DFS_SPECPOP", spec)
+    fabric = T.fat_tree(48) if name == "fat_tree_k48" else T.dragonfly(16, 8, 8)
+    csr = fabric.csr()
+    srcs = np.unique(fabric.host_table()[0]).astype(np.int32)[:nsrc]
+    ctx.upload(csr)
+    tree = ctx.dfs_tables_packed(srcs)
+    assert ctx.last_kernel().startswith("dfs_async_kernel<")
+    po, to, _ = O.dfs_tables(csr, srcs, with_hops=False, nthreads=NTHREADS)
+    np.testing.assert_array_equal(tree, _pack(po, to))
+
+
+@pytest.mark.parametrize("spec", ["default", "1"])
 @pytest.mark.parametrize("c16", ["0", "1", "0plain", "1plain"])
 @pytest.mark.parametrize("layout", ["int32", "hops"])
 @pytest.mark.parametrize("name", G.SMALL)
-def test_dfs_async_compact_lds(ctx, monkeypatch, name, layout, c16):
+def test_dfs_async_compact_lds(ctx, monkeypatch, name, layout, c16, spec):
     """dfs_async_kernel with the compact LDS layout (u16 counts in pairs, u16
     parents + u8 slots; the dragonfly default) and without -- with the
     workers' pre-swizzled in-rows (the default) or the plain ones -- every
     source."""
     _strategy(monkeypatch, "async")
+    if spec != "default":
+        monkeypatch.setenv("SDNROUTE_DFS_SPECPOP", spec)
     monkeypatch.setenv("SDNROUTE_DFS_C16", c16[0])
     if c16.endswith("plain"):
         monkeypatch.setenv("SDNROUTE_DFS_PRESWZ", "0")
