@@ -2690,8 +2690,11 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         const char *pz = getenv("SDNROUTE_DFS_PRESWZ");
         const uint16_t *rw = c16 ? ctx->radjc : ctx->radjw;
         const bool preswz = rw && !(pz && !strcmp(pz, "0"));
-        // speculative stack pops (SDNROUTE_DFS_SPECPOP=0|1)
-        bool specpop = false;
+        // speculative stack pops (SDNROUTE_DFS_SPECPOP=0|1), same box, two
+        // runs (gpurun_out/r5_k): k=48 1,152 sources 90.8 / 91.2 -> 90.4 /
+        // 90.5 us, 144 sources 56.4 -> 55.5 us, one source 53.7 -> 53.4 us,
+        // dragonfly 195.8 -> 192.9 us
+        bool specpop = true;
         if (const char *f = getenv("SDNROUTE_DFS_SPECPOP")) specpop = !strcmp(f, "1");
         const int aflags = dfs_flags(kFlagPrio) | (preswz ? kFlagPreSwz : 0) | hflags |
                            (specpop ? kFlagSpecPop : 0);
