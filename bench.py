@@ -326,15 +326,17 @@ def materialised_flows(ctx, dev, stream, csr, fabric, srcs, chunk=1 << 24, packe
     sw = torch.empty(chunk * max_len, dtype=torch.int32, device=dev)
     hpo = sw if packed else torch.empty_like(sw)
 
-    def expand(rows, dsts, last, n):
+    def expand(rows, dsts, last, n, same=False):
+        # same: the tables of the previous chunk -- the walk tables derived
+        # from them (packed trees + ancestor tables) are built once per pass
         if packed:
             ctx.expand_routes_packed_device(par.data_ptr(), prt.data_ptr(), S, rows.data_ptr(),
                                             dsts.data_ptr(), last.data_ptr(), n, off.data_ptr(),
-                                            sw.data_ptr())
+                                            sw.data_ptr(), same_tables=same)
         else:
             ctx.expand_routes_device(par.data_ptr(), prt.data_ptr(), S, rows.data_ptr(),
                                      dsts.data_ptr(), last.data_ptr(), n, off.data_ptr(),
-                                     sw.data_ptr(), hpo.data_ptr())
+                                     sw.data_ptr(), hpo.data_ptr(), same_tables=same)
     reqs = []                                   # (rows, dsts, last) per chunk, untimed
     for p0 in range(0, npairs, chunk):
         idx = torch.arange(p0, min(npairs, p0 + chunk), dtype=torch.int64, device=dev)
@@ -360,11 +362,11 @@ def materialised_flows(ctx, dev, stream, csr, fabric, srcs, chunk=1 << 24, packe
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
-    for rows, dsts, last in reqs:
+    for c, (rows, dsts, last) in enumerate(reqs):
         n = rows.shape[0]
         ctx.route_offsets_device(hop.data_ptr(), rows.data_ptr(), dsts.data_ptr(), n,
                                  off.data_ptr(), nrows=S)
-        expand(rows, dsts, last, n)
+        expand(rows, dsts, last, n, same=c > 0)  # walk tables built in the first chunk
         entries += off[n]                        # stream-ordered, no host sync
     e1.record(stream)
     torch.cuda.synchronize(dev)

@@ -43,6 +43,10 @@ extern "C" {
 
 #define SDNR_DEVICE_PTRS 0x1u /* table/source pointers are device pointers */
 #define SDNR_TIMING      0x2u /* time the main kernel (sdnr_last_kernel_ms) */
+#define SDNR_SAME_TABLES 0x4u /* route expansion: the parent / port tables are the
+                                 ones (same pointers, same contents) of the
+                                 previous expansion on this context -- its
+                                 derived walk tables are reused */
 
 #define SDNR_UNREACHED (-1)
 #define SDNR_DIST_INF  0xFFFFu

@@ -139,6 +139,7 @@ static void free_graph(sdnr_ctx *c)
     c->radj_pair = false;
     c->V = -1;
     c->E = 0;
+    c->anc_valid = false;                // derived walk tables follow the graph
     c->W = 0;
     c->max_deg = 0;
 }
@@ -319,6 +320,7 @@ int sdnr_destroy(sdnr_ctx *ctx)
     if (ctx->scratch2) (void)hipFree(ctx->scratch2);
     if (ctx->wq) (void)hipFree(ctx->wq);
     if (ctx->dmat) (void)hipFree(ctx->dmat);
+    if (ctx->anc) (void)hipFree(ctx->anc);
     if (ctx->stage) (void)hipFree(ctx->stage);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->h_flag) (void)hipHostFree(ctx->h_flag);
@@ -1087,7 +1089,8 @@ int sdnr_route_expand_packed(sdnr_ctx *ctx, const int32_t *parent, const int32_t
         (npairs > 0 && (!parent || !port || !rows || !dsts || !last_port || !entries)))
         return sdnr_fail(SDNR_ERR_INVAL, "sdnr_route_expand_packed: bad arguments");
     return sdnr_launch_route_expand(ctx, parent, port, nrows, rows, dsts, last_port, npairs,
-                                    offsets, nullptr, nullptr, entries);
+                                    offsets, nullptr, nullptr, entries,
+                                    (flags & SDNR_SAME_TABLES) != 0);
 }
 
 int sdnr_route_expand(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port, int32_t nrows,
@@ -1102,7 +1105,8 @@ int sdnr_route_expand(sdnr_ctx *ctx, const int32_t *parent, const int32_t *port,
         return sdnr_fail(SDNR_ERR_INVAL, "sdnr_route_expand: bad arguments");
     if (flags & SDNR_DEVICE_PTRS)
         return sdnr_launch_route_expand(ctx, parent, port, nrows, rows, dsts, last_port, npairs,
-                                        offsets, hop_switch, hop_port);
+                                        offsets, hop_switch, hop_port, nullptr,
+                                        (flags & SDNR_SAME_TABLES) != 0);
     if ((rc = check_pairs(ctx, nrows, rows, dsts, npairs, "sdnr_route_expand"))) return rc;
     const int64_t total = offsets[npairs];
     if (total > 0 && (!hop_switch || !hop_port))

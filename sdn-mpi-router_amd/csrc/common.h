@@ -88,6 +88,13 @@ struct sdnr_ctx {
     size_t wq_bytes = 0;
     void *dmat = nullptr;               // V x V distances behind APSP-derived shortest tables
     size_t dmat_bytes = 0;
+    // the route expansion's walk tables (packed trees + u16 ancestor tables)
+    // and what they were built from (SDNR_SAME_TABLES reuses them)
+    void *anc = nullptr;
+    size_t anc_bytes = 0;
+    const void *anc_parent = nullptr, *anc_port = nullptr;
+    size_t anc_n = 0;
+    bool anc_valid = false;
     bool port16 = false;                // every port fits the packed layout (< 0xFFFF)
     bool symmetric = false;             // every link (u, v) has its reverse (v, u)
 
@@ -185,7 +192,8 @@ int sdnr_launch_route_offsets(sdnr_ctx *ctx, const int32_t *d_hops, const int32_
 int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32_t *d_port,
                              int32_t nrows, const int32_t *d_rows, const int32_t *d_dsts,
                              const int32_t *d_last_port, int32_t npairs, const int64_t *d_off,
-                             int32_t *d_switch, int32_t *d_hport, uint32_t *d_entries = nullptr);
+                             int32_t *d_switch, int32_t *d_hport, uint32_t *d_entries = nullptr,
+                             bool same_tables = false);
 // rows of cached default-route trees a link change alters (incremental.hip)
 int sdnr_launch_dfs_rows_affected(sdnr_ctx *ctx, const uint32_t *d_tree, const void *d_depth,
                                   int32_t layout, int32_t depth_bytes, int32_t nrows,

@@ -982,7 +982,8 @@ int sdnr_launch_route_offsets(sdnr_ctx *ctx, const int32_t *d_hops, const int32_
 int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32_t *d_port,
                              int32_t nrows, const int32_t *d_rows, const int32_t *d_dsts,
                              const int32_t *d_last_port, int32_t npairs, const int64_t *d_off,
-                             int32_t *d_switch, int32_t *d_hport, uint32_t *d_entries)
+                             int32_t *d_switch, int32_t *d_hport, uint32_t *d_entries,
+                             bool same_tables)
 {
     if (npairs == 0) return SDNR_OK;
     if (d_entries && !(ctx->V <= 0xFFFF && ctx->port16))
@@ -990,31 +991,37 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
     const char *f = getenv("SDNROUTE_ROUTE_WALK");      // "serial": one lane per pair
     const bool serial = f && !strcmp(f, "serial");
     const size_t n = (size_t)nrows * (size_t)ctx->V;
-    int32_t *anc = nullptr, *tmp = nullptr;
-    if (!serial) {
-        int rc = sdnr_reserve(&ctx->scratch2, &ctx->scratch2_bytes, 14 * n + 64);
-        if (rc) return rc;
-        anc = static_cast<int32_t *>(ctx->scratch2);
-        tmp = anc + n;
-    }
     if (ctx->timed) SDNR_HIP(hipEventRecord(ctx->ev0, ctx->stream));
     const char *pk = getenv("SDNROUTE_ROUTE_PACKED");          // "0": int32 tables
     const bool packed = d_entries ||
                         (!serial && ctx->V <= 0xFFFF && ctx->port16 && !(pk && !strcmp(pk, "0")));
     if (packed) {
-        // scratch2 (14n bytes): tree u32 [n] | u16 ancestor tables a1..a16 [n]
-        uint32_t *tree = reinterpret_cast<uint32_t *>(anc);
+        // walk tables (14n bytes, a buffer of their own): tree u32 [n] | u16
+        // ancestor tables a1..a16 [n]; rebuilt unless the caller says the
+        // tables are the previous call's (SDNR_SAME_TABLES) and they match
+        const bool reuse = same_tables && ctx->anc_valid && ctx->anc_parent == d_parent &&
+                           ctx->anc_port == d_port && ctx->anc_n == n;
+        if (!reuse) {
+            int rc = sdnr_reserve(&ctx->anc, &ctx->anc_bytes, 14 * n + 64);
+            if (rc) return rc;
+        }
+        uint32_t *tree = static_cast<uint32_t *>(ctx->anc);
         uint16_t *a16 = reinterpret_cast<uint16_t *>(tree + n);
         const int cg = ctx->num_cus * 8;
-        hipLaunchKernelGGL(tree_pack_kernel, dim3(cg), dim3(256), 0, ctx->stream, n, d_parent,
-                           d_port, tree, a16);
         Anc16 tabs{};
-        for (int j = 1; j <= 4; ++j) {
-            uint16_t *o = a16 + (size_t)j * n;
-            const uint16_t *prev = a16 + (size_t)(j - 1) * n;
-            hipLaunchKernelGGL(tree_compose16_kernel, dim3(cg), dim3(256), 0, ctx->stream,
-                               ctx->V, n, prev, prev, o);
-            tabs.a[j] = o;
+        for (int j = 1; j <= 4; ++j) tabs.a[j] = a16 + (size_t)j * n;
+        if (!reuse) {
+            hipLaunchKernelGGL(tree_pack_kernel, dim3(cg), dim3(256), 0, ctx->stream, n, d_parent,
+                               d_port, tree, a16);
+            for (int j = 1; j <= 4; ++j) {
+                const uint16_t *prev = a16 + (size_t)(j - 1) * n;
+                hipLaunchKernelGGL(tree_compose16_kernel, dim3(cg), dim3(256), 0, ctx->stream,
+                                   ctx->V, n, prev, prev, a16 + (size_t)j * n);
+            }
+            ctx->anc_parent = d_parent;
+            ctx->anc_port = d_port;
+            ctx->anc_n = n;
+            ctx->anc_valid = true;
         }
         const char *sg = getenv("SDNROUTE_ROUTE_SEG");        // "0": per-entry jump walks
         if (d_entries || !(sg && !strcmp(sg, "0"))) {
@@ -1129,6 +1136,11 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
         hipLaunchKernelGGL(route_walk_kernel, dim3(g), dim3(256), 0, ctx->stream, ctx->V, d_parent,
                            d_port, d_rows, d_dsts, d_last_port, npairs, d_off, d_switch, d_hport);
     } else {
+        // int32 ancestor tables in scratch2 (2 x n int32)
+        int rc = sdnr_reserve(&ctx->scratch2, &ctx->scratch2_bytes, 8 * n + 64);
+        if (rc) return rc;
+        int32_t *anc = static_cast<int32_t *>(ctx->scratch2);
+        int32_t *tmp = anc + n;
         // P-th ancestors by doubling: p2 = p o p, p4 = p2 o p2, ...
         // SDNROUTE_ROUTE_P=4|8|16 lanes per pair (default 16: k=48 1M rank
         // pairs 0.57 ms at 8, 0.54 ms at 16, 0.75 ms at 4)

@@ -24,6 +24,7 @@ _LIB_NAME = "libsdnroute.so"
 
 DEVICE_PTRS = 0x1
 TIMING = 0x2
+SAME_TABLES = 0x4        # route expansion: the previous call's parent / port tables
 UNREACHED = -1
 DIST_INF = 0xFFFF
 TREE_NONE = 0xFFFFFFFF
@@ -371,8 +372,8 @@ class Context(object):
                                             int(npairs), ctypes.c_void_p(off_ptr), DEVICE_PTRS))
 
     def expand_routes_device(self, parent_ptr, port_ptr, nrows, rows_ptr, dsts_ptr, last_ptr,
-                             npairs, off_ptr, sw_ptr, hp_ptr, timing=False):
-        flags = DEVICE_PTRS | (TIMING if timing else 0)
+                             npairs, off_ptr, sw_ptr, hp_ptr, timing=False, same_tables=False):
+        flags = DEVICE_PTRS | (TIMING if timing else 0) | (SAME_TABLES if same_tables else 0)
         _check(self._lib.sdnr_route_expand(self._h, ctypes.c_void_p(parent_ptr),
                                            ctypes.c_void_p(port_ptr), int(nrows),
                                            ctypes.c_void_p(rows_ptr),
@@ -381,10 +382,13 @@ class Context(object):
                                            ctypes.c_void_p(sw_ptr), ctypes.c_void_p(hp_ptr), flags))
 
     def expand_routes_packed_device(self, parent_ptr, port_ptr, nrows, rows_ptr, dsts_ptr,
-                                    last_ptr, npairs, off_ptr, ent_ptr, timing=False):
+                                    last_ptr, npairs, off_ptr, ent_ptr, timing=False,
+                                    same_tables=False):
         """Flow entries as one u32 each, switch | port << 16
-        (sdnr_route_expand_packed, device pointers)."""
-        flags = DEVICE_PTRS | (TIMING if timing else 0)
+        (sdnr_route_expand_packed, device pointers).  same_tables: the
+        parent / port tables of the previous expansion on this context
+        (SDNR_SAME_TABLES: its walk tables are reused)."""
+        flags = DEVICE_PTRS | (TIMING if timing else 0) | (SAME_TABLES if same_tables else 0)
         _check(self._lib.sdnr_route_expand_packed(
             self._h, ctypes.c_void_p(parent_ptr), ctypes.c_void_p(port_ptr), int(nrows),
             ctypes.c_void_p(rows_ptr), ctypes.c_void_p(dsts_ptr), ctypes.c_void_p(last_ptr),

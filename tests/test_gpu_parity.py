@@ -932,6 +932,68 @@ def test_route_expand_packed_rejects_wide_last_port(ctx):
             assert ei.value.code == -22 and "last port" in str(ei.value)
 
 
+@pytest.mark.parametrize("packed", [True, False])
+def test_route_expand_same_tables(ctx, packed):
+    """SDNR_SAME_TABLES: chunks of pairs over one set of tables reuse the
+    walk tables the first chunk built; tables at other addresses, or the same
+    addresses without the flag, are rebuilt.  Every chunk's entries equal the
+    host path's (which always rebuilds)."""
+    import torch
+    csr = T.fat_tree(8).csr()
+    ctx.upload(csr)
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(11)
+    srcs = np.arange(csr.V, dtype=np.int32)
+    tabs = []
+    for perm in (srcs, rng.permutation(srcs).astype(np.int32)):
+        par, prt, hop = O.dfs_tables(csr, perm, nthreads=NTHREADS)
+        tabs.append((par, prt, hop))
+
+    def run(t_host, t_dev, same, n=5000):
+        par, prt, hop = t_host
+        rows = rng.integers(0, csr.V, n).astype(np.int32)
+        dsts = rng.integers(0, csr.V, n).astype(np.int32)
+        last = rng.integers(1, 200, n).astype(np.int32)
+        off, sw, hp = ctx.expand_routes(par, prt, hop, rows, dsts, last)
+        r, d, l = (torch.from_numpy(a).to(dev) for a in (rows, dsts, last))
+        doff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        ctx.route_offsets_device(t_dev[2].data_ptr(), r.data_ptr(), d.data_ptr(), n,
+                                 doff.data_ptr(), nrows=csr.V)
+        tot = int(off[-1])
+        if packed:
+            ent = torch.zeros(tot, dtype=torch.int32, device=dev)
+            ctx.expand_routes_packed_device(t_dev[0].data_ptr(), t_dev[1].data_ptr(), csr.V,
+                                            r.data_ptr(), d.data_ptr(), l.data_ptr(), n,
+                                            doff.data_ptr(), ent.data_ptr(), same_tables=same)
+            ctx.synchronize()
+            e = ent.cpu().numpy().view(np.uint32)
+            np.testing.assert_array_equal(e & 0xFFFF, sw)
+            np.testing.assert_array_equal(e >> 16, hp)
+        else:
+            dsw = torch.zeros(tot, dtype=torch.int32, device=dev)
+            dhp = torch.zeros(tot, dtype=torch.int32, device=dev)
+            ctx.expand_routes_device(t_dev[0].data_ptr(), t_dev[1].data_ptr(), csr.V,
+                                     r.data_ptr(), d.data_ptr(), l.data_ptr(), n,
+                                     doff.data_ptr(), dsw.data_ptr(), dhp.data_ptr(),
+                                     same_tables=same)
+            ctx.synchronize()
+            np.testing.assert_array_equal(dsw.cpu().numpy(), sw)
+            np.testing.assert_array_equal(dhp.cpu().numpy(), hp)
+        np.testing.assert_array_equal(doff.cpu().numpy(), off)
+
+    da = [torch.from_numpy(a).to(dev) for a in tabs[0]]
+    db = [torch.from_numpy(a).to(dev) for a in tabs[1]]
+    run(tabs[0], da, False)
+    for _ in range(3):
+        run(tabs[0], da, True)                   # reused
+    run(tabs[1], db, True)                       # other addresses: rebuilt
+    run(tabs[1], db, True)
+    for i in range(3):                           # same addresses, new contents, no flag
+        da[i].copy_(db[i])
+    run(tabs[1], da, False)
+    run(tabs[1], da, True)
+
+
 @pytest.mark.parametrize("scan", ["fused", "4"])
 @pytest.mark.parametrize("npairs", [1, 8191, 8192, 8193, 3_000_000])
 def test_route_offsets_scan(ctx, monkeypatch, scan, npairs):
