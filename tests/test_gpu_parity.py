@@ -568,6 +568,7 @@ def test_shortest_plane_repeated_destinations(ctx, monkeypatch, dp, init):
         dist = torch.zeros((n, V), dtype=torch.int16, device=dev)
         nh = torch.zeros((n, V), dtype=torch.int32, device=dev)
         nhp = torch.zeros_like(nh)
+        torch.cuda.synchronize(dev)      # torch's fills run on torch's stream
         ctx.shortest_tables_device(td.data_ptr(), n, dist.data_ptr(), nh.data_ptr(),
                                    nhp.data_ptr())
         ctx.synchronize()
@@ -654,6 +655,7 @@ def test_shortest_unknown_destination_rows_device(ctx):
     dist = torch.zeros((3, csr.V), dtype=torch.int16, device=dev)
     nh = torch.zeros((3, csr.V), dtype=torch.int32, device=dev)
     nhp = torch.zeros_like(nh)
+    torch.cuda.synchronize(dev)          # torch's fills run on torch's stream
     ctx.shortest_tables_device(td.data_ptr(), 3, dist.data_ptr(), nh.data_ptr(), nhp.data_ptr())
     ctx.synchronize()
     d = dist.cpu().numpy().view(np.uint16)
@@ -912,12 +914,14 @@ def test_route_expand_packed_rejects_wide_last_port(ctx):
     rows = torch.tensor([0, 1, 2], dtype=torch.int32, device=dev)
     dsts = torch.tensor([5, 6, 7], dtype=torch.int32, device=dev)
     off = torch.empty(4, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
     ctx.route_offsets_device(th.data_ptr(), rows.data_ptr(), dsts.data_ptr(), 3, off.data_ptr(),
                              nrows=csr.V)
     ctx.synchronize()
     ent = torch.zeros(int(off[-1].item()), dtype=torch.int32, device=dev)
     for bad, ok in (([1, 70000, 2], False), ([1, -1, 2], False), ([1, 0xFFFE, 2], True)):
         last = torch.tensor(bad, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize(dev)      # torch's copies / fills run on torch's stream
         ctx.expand_routes_packed_device(tp.data_ptr(), tt.data_ptr(), csr.V, rows.data_ptr(),
                                         dsts.data_ptr(), last.data_ptr(), 3, off.data_ptr(),
                                         ent.data_ptr())
@@ -957,11 +961,13 @@ def test_route_expand_same_tables(ctx, packed):
         off, sw, hp = ctx.expand_routes(par, prt, hop, rows, dsts, last)
         r, d, l = (torch.from_numpy(a).to(dev) for a in (rows, dsts, last))
         doff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize(dev)      # torch's copies / fills run on torch's stream
         ctx.route_offsets_device(t_dev[2].data_ptr(), r.data_ptr(), d.data_ptr(), n,
                                  doff.data_ptr(), nrows=csr.V)
         tot = int(off[-1])
         if packed:
             ent = torch.zeros(tot, dtype=torch.int32, device=dev)
+            torch.cuda.synchronize(dev)
             ctx.expand_routes_packed_device(t_dev[0].data_ptr(), t_dev[1].data_ptr(), csr.V,
                                             r.data_ptr(), d.data_ptr(), l.data_ptr(), n,
                                             doff.data_ptr(), ent.data_ptr(), same_tables=same)
@@ -972,6 +978,7 @@ def test_route_expand_same_tables(ctx, packed):
         else:
             dsw = torch.zeros(tot, dtype=torch.int32, device=dev)
             dhp = torch.zeros(tot, dtype=torch.int32, device=dev)
+            torch.cuda.synchronize(dev)
             ctx.expand_routes_device(t_dev[0].data_ptr(), t_dev[1].data_ptr(), csr.V,
                                      r.data_ptr(), d.data_ptr(), l.data_ptr(), n,
                                      doff.data_ptr(), dsw.data_ptr(), dhp.data_ptr(),
@@ -990,8 +997,73 @@ def test_route_expand_same_tables(ctx, packed):
     run(tabs[1], db, True)
     for i in range(3):                           # same addresses, new contents, no flag
         da[i].copy_(db[i])
+    torch.cuda.synchronize(dev)
     run(tabs[1], da, False)
     run(tabs[1], da, True)
+
+
+@pytest.mark.parametrize("pipe", ["default", "4,4,2", "0"])
+def test_route_expand_k48_large_batch(ctx, monkeypatch, pipe):
+    """A 4.3 M-pair batch on k=48 -- the all-pairs order of the materialised
+    flows (runs of 24 hosts per destination switch, DFS routes of ~70
+    entries) followed by random pairs and same-switch pairs: the u32 entries
+    of the default large-batch kernel (route_seg_pipe_kernel, walker and
+    storer waves), of another shape and of the one-role kernel
+    (SDNROUTE_ROUTE_PIPE=0) equal the int32 switch / port arrays of
+    route_seg_packed_kernel, and a sample of pairs equals the host path's
+    entries."""
+    import torch
+    if pipe != "default":
+        monkeypatch.setenv("SDNROUTE_ROUTE_PIPE", pipe)
+    fabric = T.fat_tree(48)
+    csr = fabric.csr()
+    ctx.upload(csr)
+    dev = torch.device("cuda", 0)
+    hv, hp = fabric.host_table()
+    srcs = np.unique(hv).astype(np.int32)
+    H = len(hv)
+    par, prt, hop = ctx.dfs_tables(srcs)
+    tp, tt, th = (torch.from_numpy(a).to(dev) for a in (par, prt, hop))
+    rng = np.random.default_rng(5)
+    n_ord = (1 << 22) + 4321
+    idx = np.arange(3 * H + 17, 3 * H + 17 + n_ord, dtype=np.int64)
+    a = np.concatenate([idx // H, rng.integers(0, H, 200_000), np.full(500, 7)])
+    b = np.concatenate([idx % H, rng.integers(0, H, 200_000), np.full(500, 7)])
+    rows = np.searchsorted(srcs, hv[a]).astype(np.int32)
+    dsts = hv[b].astype(np.int32)
+    last = hp[b].astype(np.int32)
+    n = len(rows)
+    r, d, l = (torch.from_numpy(x).to(dev) for x in (rows, dsts, last))
+    off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    ctx.route_offsets_device(th.data_ptr(), r.data_ptr(), d.data_ptr(), n, off.data_ptr(),
+                             nrows=len(srcs))
+    ctx.synchronize()
+    tot = int(off[-1].item())
+    ent = torch.zeros(tot, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)          # torch's fill runs on its own stream, not the context's
+    ctx.expand_routes_packed_device(tp.data_ptr(), tt.data_ptr(), len(srcs), r.data_ptr(),
+                                    d.data_ptr(), l.data_ptr(), n, off.data_ptr(), ent.data_ptr())
+    ctx.synchronize()
+    assert ctx.last_kernel() == ("route_seg_packed_kernel<1024,u32>" if pipe == "0"
+                                 else "route_seg_pipe_kernel<u32>")
+    sw = torch.zeros(tot, dtype=torch.int32, device=dev)
+    pt = torch.zeros(tot, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    monkeypatch.delenv("SDNROUTE_ROUTE_PIPE", raising=False)   # the int32 one-role kernel
+    ctx.expand_routes_device(tp.data_ptr(), tt.data_ptr(), len(srcs), r.data_ptr(), d.data_ptr(),
+                             l.data_ptr(), n, off.data_ptr(), sw.data_ptr(), pt.data_ptr())
+    ctx.synchronize()
+    assert ctx.last_kernel() == "route_seg_packed_kernel<1024>"
+    e = ent.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(e & 0xFFFF, sw.cpu().numpy())
+    np.testing.assert_array_equal(e >> 16, pt.cpu().numpy())
+    o = off.cpu().numpy()
+    pick = np.concatenate([rng.integers(0, n, 3000), [0, n - 1, n_ord - 1, n_ord]])
+    so, ssw, shp = ctx.expand_routes(par, prt, hop, rows[pick], dsts[pick], last[pick])
+    for j, i in enumerate(pick):
+        np.testing.assert_array_equal(e[o[i]:o[i + 1]] & 0xFFFF, ssw[so[j]:so[j + 1]])
+        np.testing.assert_array_equal(e[o[i]:o[i + 1]] >> 16, shp[so[j]:so[j + 1]])
 
 
 @pytest.mark.parametrize("scan", ["fused", "4"])
