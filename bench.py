@@ -923,6 +923,15 @@ def main():
     inflight = args.inflight if args.inflight > 0 else \
         (1 if world == 1 else max(1, min(3, -(-4 * cus // max(1, per)))))
     streams = [stream] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
+    # one library context per stream in flight: a context's scratch (the split
+    # kernel's spill rings and chunk cursors, the watchdog word) serves one
+    # stream at a time
+    ctxs = [ctx]
+    for st in streams[1:]:
+        c = _native.Context(local)
+        c.upload(csr)
+        c.set_stream(st.cuda_stream)
+        ctxs.append(c)
     nbuf = (2 if world > 1 else 1) * inflight
     bufs = [tables() for _ in range(nbuf)]
     gathered = [tuple(torch.empty((world * per, V), dtype=t.dtype, device=dev) for t in b)
@@ -934,25 +943,24 @@ def main():
     def step(ev=None):
         k = counter[0] % nbuf
         st = streams[counter[0] % inflight]   # table set k always runs on stream k % inflight
+        cx = ctxs[counter[0] % inflight]      # ... through that stream's context
         counter[0] += 1
         with torch.cuda.stream(st):
             for w in pending[k]:            # this set's previous gather is done
                 w.wait()
             pending[k] = []
             tb = bufs[k]
-            if inflight > 1:
-                ctx.set_stream(st.cuda_stream)
             if ev is not None:
                 ev[0].record(st)
             if slots:
-                ctx.dfs_tables_slots_device(t_src.data_ptr(), per, tb[0].data_ptr())
+                cx.dfs_tables_slots_device(t_src.data_ptr(), per, tb[0].data_ptr())
             elif packed:
-                ctx.dfs_tables_packed_device(t_src.data_ptr(), per, tb[0].data_ptr())
+                cx.dfs_tables_packed_device(t_src.data_ptr(), per, tb[0].data_ptr())
             elif args.mode == "dfs":
-                ctx.dfs_tables_device(t_src.data_ptr(), per, tb[0].data_ptr(), tb[1].data_ptr())
+                cx.dfs_tables_device(t_src.data_ptr(), per, tb[0].data_ptr(), tb[1].data_ptr())
             else:
-                ctx.shortest_tables_device(t_src.data_ptr(), per, tb[0].data_ptr(),
-                                           tb[1].data_ptr(), tb[2].data_ptr())
+                cx.shortest_tables_device(t_src.data_ptr(), per, tb[0].data_ptr(),
+                                          tb[1].data_ptr(), tb[2].data_ptr())
             if ev is not None:
                 ev[1].record(st)
             if world > 1:                   # assemble [sources][V] on every rank / rank 0
@@ -982,7 +990,8 @@ def main():
         step(evs[i] if i % every == 0 else None)
     drain()
     torch.cuda.synchronize(dev)
-    ctx.synchronize()          # raises if a kernel's bounded wait tripped: tables invalid
+    for c in ctxs:
+        c.synchronize()        # raises if a kernel's bounded wait tripped: tables invalid
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -1001,6 +1010,8 @@ def main():
         multi = multi_gpu_extras(args, world, rank, local, dev, csr, srcs, per, packed, slots,
                                  kern_ms, ms_per_step, routes, step, drain, bufs, gathered,
                                  assemble)
+    for c in ctxs[1:]:
+        c.close()
     bytes_launch = algorithmic_bytes_per_source(V, E, args.mode, packed) * (hi - lo)
     achieved = bytes_launch / (kern_ms / 1e3) / 1e9
     per_entry = (4 if packed else 8) if args.mode == "dfs" else 10
