@@ -848,13 +848,13 @@ def main():
         # forks: must run before the first GPU call of this process
         ref_mp = cpu_reference_path_mp(T.by_name(args.fabric),
                                        secs=min(5.0, args.cpu_budget_s / 4))
-    if world > 1:
+    torch.cuda.set_device(local)              # before the process group: its communicator
+    if world > 1:                             # and every context live on this rank's GPU
         backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")   # gloo: rehearsal only
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     devices = None
     if world > 1:
