@@ -688,7 +688,8 @@ __global__ __launch_bounds__((NWK + NST) * 64) void route_seg_pipe_kernel(
     int V, const uint32_t *__restrict__ tree, Anc16 anc,
     const int32_t *__restrict__ rows, const int32_t *__restrict__ dsts,
     const int32_t *__restrict__ last_port, int npairs, const int64_t *__restrict__ off,
-    int32_t *__restrict__ hop_switch, int32_t *__restrict__ hop_port, int *__restrict__ err)
+    int32_t *__restrict__ hop_switch, int32_t *__restrict__ hop_port, int *__restrict__ err,
+    int diag)
 {
     static_assert(NWK % NST == 0, "each storer serves NWK / NST walkers");
     constexpr unsigned kSpin = 1u << 24;
@@ -783,7 +784,8 @@ __global__ __launch_bounds__((NWK + NST) * 64) void route_seg_pipe_kernel(
                 }
                 SegSlot<CAP> &sl = slots[w * NSL + P % NSL];
                 // distinct paths of the n pairs, 4 at a time (16 lanes each)
-                uint64_t heads = __ballot(head && lane < n && pl > 0);
+                // (diag 1, timing only: no route walks)
+                uint64_t heads = (diag & 1) ? 0ull : __ballot(head && lane < n && pl > 0);
                 while (heads) {
                     const int q = lane >> 4, k = lane & 15;
                     uint64_t hm = heads;
@@ -851,7 +853,8 @@ __global__ __launch_bounds__((NWK + NST) * 64) void route_seg_pipe_kernel(
             progress = true;
             const SegSlot<CAP> &sl = slots[ww * NSL + C[q] % NSL];
             const int n = sl.n;
-            uint64_t runs = (uint64_t)sl.mlo | ((uint64_t)sl.mhi << 32);
+            // (diag 2, timing only: no entry stores)
+            uint64_t runs = (diag & 2) ? 0ull : ((uint64_t)sl.mlo | ((uint64_t)sl.mhi << 32));
             while (runs) {
                 const int p0 = __builtin_ctzll(runs);
                 runs &= runs - 1;
@@ -1099,7 +1102,7 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
                         !(nt && !strcmp(nt, "1")) && !diag;
             if (const char *pp = getenv("SDNROUTE_ROUTE_PIPE")) {
                 if (!strcmp(pp, "0")) pipe = false;
-                else if (sscanf(pp, "%d,%d,%d", &pw, &ps, &pn) == 3) pipe = !diag;
+                else if (sscanf(pp, "%d,%d,%d", &pw, &ps, &pn) == 3) pipe = true;   // diag too
             }
             if (pipe) {
                 bool launched = false;
@@ -1115,11 +1118,11 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
             hipLaunchKernelGGL((route_seg_pipe_kernel<512, true, W_, S_, N_>), dim3((unsigned)pg), \
                                dim3((W_ + S_) * 64), 0, ctx->stream, ctx->V, tree, tabs, d_rows, \
                                d_dsts, d_last_port, npairs, d_off,                           \
-                               reinterpret_cast<int32_t *>(d_entries), nullptr, ctx->d_err);  \
+                               reinterpret_cast<int32_t *>(d_entries), nullptr, ctx->d_err, diag); \
         else                                                                                 \
             hipLaunchKernelGGL((route_seg_pipe_kernel<512, false, W_, S_, N_>), dim3((unsigned)pg), \
                                dim3((W_ + S_) * 64), 0, ctx->stream, ctx->V, tree, tabs, d_rows, \
-                               d_dsts, d_last_port, npairs, d_off, d_switch, d_hport, ctx->d_err); \
+                               d_dsts, d_last_port, npairs, d_off, d_switch, d_hport, ctx->d_err, diag); \
         launched = true;                                                                     \
     }
                 SDNR_PIPE(4, 2, 2)

@@ -44,6 +44,36 @@ __global__ __launch_bounds__(256) void group_kernel(uint4 *o, size_t ngroups, in
     }
 }
 
+// runs: the expansion's real pattern -- a group is a sequence of runs of
+// `run` 4-B entries starting at arbitrary 4-B offsets; each run is stored
+// as the seg kernels do: up to 3 single entries to the 16-B boundary, 16-B
+// stores, up to 3 single entries at the end (RUNFLAT: the same group stored
+// as one range, head and tail once per group)
+template <bool RUNFLAT>
+__global__ __launch_bounds__(256) void runs_kernel(uint32_t *o, size_t ngroups, int per_group,
+                                                   int run)
+{
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const size_t nwaves = (size_t)gridDim.x * 4;
+    for (size_t g = blockIdx.x * 4 + wv; g < ngroups; g += nwaves) {
+        const size_t gbase = g * (size_t)per_group + 1;      // groups start 4 B past a boundary
+        const int len = per_group - 2;
+        for (int r0 = 0; r0 < len; r0 += RUNFLAT ? len : run) {
+            const int total = RUNFLAT ? len : min(run, len - r0);
+            uint32_t *p = o + gbase + r0;
+            const int hd = min(total, (int)(((16u - ((uint32_t)(uintptr_t)p & 15u)) & 15u) >> 2));
+            if (lane < hd) p[lane] = (uint32_t)lane;
+            const int bend = hd + ((total - hd) & ~3);
+            for (int t0 = hd; t0 < bend; t0 += 256) {
+                const int t = t0 + 4 * lane;
+                if (t < bend)
+                    *reinterpret_cast<uint4 *>(p + t) = make_uint4((uint32_t)t, 1u, 2u, 3u);
+            }
+            if (bend + lane < total) p[bend + lane] = 7u;
+        }
+    }
+}
+
 int main()
 {
     const size_t bytes = 4680ull << 20;
@@ -58,6 +88,24 @@ int main()
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     for (int rep = 0; rep < 3; ++rep) {
+        // the real pattern: 18,432-B groups (64 pairs x 72 entries), runs of 1,728 entries
+        const int pg = 4608, nr = (int)(bytes / 4 / pg);
+        for (int which = 0; which < 2; ++which) {
+            CK(hipEventRecord(a));
+            if (which == 0)
+                hipLaunchKernelGGL(runs_kernel<false>, dim3(cus * 8), dim3(256), 0, 0,
+                                   reinterpret_cast<uint32_t *>(o), (size_t)nr - 1, pg, 1728);
+            else
+                hipLaunchKernelGGL(runs_kernel<true>, dim3(cus * 8), dim3(256), 0, 0,
+                                   reinterpret_cast<uint32_t *>(o), (size_t)nr - 1, pg, 1728);
+            CK(hipEventRecord(b));
+            CK(hipEventSynchronize(b));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, a, b));
+            const double wb = (double)(nr - 1) * (pg - 2) * 4.0;
+            printf("%-10s %.3f ms  %.2f TB/s\n", which == 0 ? "runs" : "runs-flat", ms,
+                   wb / (ms * 1e-3) / 1e12);
+        }
         for (int which = 0; which < 3; ++which) {
             CK(hipEventRecord(a));
             if (which == 0)
