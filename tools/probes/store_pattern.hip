@@ -49,13 +49,22 @@ __global__ __launch_bounds__(256) void group_kernel(uint4 *o, size_t ngroups, in
 // as the seg kernels do: up to 3 single entries to the 16-B boundary, 16-B
 // stores, up to 3 single entries at the end (RUNFLAT: the same group stored
 // as one range, head and tail once per group)
-template <bool RUNFLAT>
+template <bool RUNFLAT, bool NT = false, bool XCD = false>
 __global__ __launch_bounds__(256) void runs_kernel(uint32_t *o, size_t ngroups, int per_group,
                                                    int run)
 {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const size_t nwaves = (size_t)gridDim.x * 4;
-    for (size_t g = blockIdx.x * 4 + wv; g < ngroups; g += nwaves) {
+    size_t nwaves = (size_t)gridDim.x * 4;
+    size_t g0 = blockIdx.x * 4 + wv, gend = ngroups;
+    if (XCD) {
+        // XCD x = block % 8 owns one contiguous eighth of the groups: the
+        // line two neighbouring groups share stays in one XCD's L2
+        const size_t x = blockIdx.x % 8, gx = (ngroups + 7) / 8;
+        nwaves = (size_t)(gridDim.x / 8) * 4;
+        g0 = x * gx + (blockIdx.x / 8) * 4 + wv;
+        gend = (x + 1) * gx < ngroups ? (x + 1) * gx : ngroups;
+    }
+    for (size_t g = g0; g < gend; g += nwaves) {
         const size_t gbase = g * (size_t)per_group + 1;      // groups start 4 B past a boundary
         const int len = per_group - 2;
         for (int r0 = 0; r0 < len; r0 += RUNFLAT ? len : run) {
@@ -66,8 +75,16 @@ __global__ __launch_bounds__(256) void runs_kernel(uint32_t *o, size_t ngroups, 
             const int bend = hd + ((total - hd) & ~3);
             for (int t0 = hd; t0 < bend; t0 += 256) {
                 const int t = t0 + 4 * lane;
-                if (t < bend)
-                    *reinterpret_cast<uint4 *>(p + t) = make_uint4((uint32_t)t, 1u, 2u, 3u);
+                if (t < bend) {
+                    if (NT) {
+                        __builtin_nontemporal_store((uint32_t)t, p + t);
+                        __builtin_nontemporal_store(1u, p + t + 1);
+                        __builtin_nontemporal_store(2u, p + t + 2);
+                        __builtin_nontemporal_store(3u, p + t + 3);
+                    } else {
+                        *reinterpret_cast<uint4 *>(p + t) = make_uint4((uint32_t)t, 1u, 2u, 3u);
+                    }
+                }
             }
             if (bend + lane < total) p[bend + lane] = 7u;
         }
@@ -90,23 +107,29 @@ int main()
     for (int rep = 0; rep < 3; ++rep) {
         // the real pattern: 18,432-B groups (64 pairs x 72 entries), runs of 1,728 entries
         const int pg = 4608, nr = (int)(bytes / 4 / pg);
-        for (int which = 0; which < 2; ++which) {
+        for (int which = 0; which < 4; ++which) {
             CK(hipEventRecord(a));
             if (which == 0)
                 hipLaunchKernelGGL(runs_kernel<false>, dim3(cus * 8), dim3(256), 0, 0,
                                    reinterpret_cast<uint32_t *>(o), (size_t)nr - 1, pg, 1728);
-            else
+            else if (which == 1)
                 hipLaunchKernelGGL(runs_kernel<true>, dim3(cus * 8), dim3(256), 0, 0,
+                                   reinterpret_cast<uint32_t *>(o), (size_t)nr - 1, pg, 1728);
+            else if (which == 2)
+                hipLaunchKernelGGL((runs_kernel<false, true>), dim3(cus * 8), dim3(256), 0, 0,
+                                   reinterpret_cast<uint32_t *>(o), (size_t)nr - 1, pg, 1728);
+            else
+                hipLaunchKernelGGL((runs_kernel<false, false, true>), dim3(cus * 8), dim3(256), 0, 0,
                                    reinterpret_cast<uint32_t *>(o), (size_t)nr - 1, pg, 1728);
             CK(hipEventRecord(b));
             CK(hipEventSynchronize(b));
             float ms = 0;
             CK(hipEventElapsedTime(&ms, a, b));
             const double wb = (double)(nr - 1) * (pg - 2) * 4.0;
-            printf("%-10s %.3f ms  %.2f TB/s\n", which == 0 ? "runs" : "runs-flat", ms,
+            printf("%-10s %.3f ms  %.2f TB/s\n", which == 0 ? "runs" : which == 1 ? "runs-flat" : which == 2 ? "runs-nt" : "runs-xcd", ms,
                    wb / (ms * 1e-3) / 1e12);
         }
-        for (int which = 0; which < 3; ++which) {
+        for (int which = 0; which < 4; ++which) {
             CK(hipEventRecord(a));
             if (which == 0)
                 hipLaunchKernelGGL(fill_kernel, dim3(cus * 8), dim3(256), 0, 0, o, bytes / 16);
