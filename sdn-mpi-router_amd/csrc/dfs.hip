@@ -1599,7 +1599,12 @@ __device__ __forceinline__ int swz(int x) { return lds_swz(x); }   // common.h
 // 0..31 child 2g and 32..63 child 2g + 1, two ds_sub per lane -- half the
 // load instructions and half the returned dwords of PAIR 0 (the CU's
 // vector-memory data return is 71 % busy at the k=48 headline's load)
-template <int NW, bool HOPS, bool PACKED, bool C16, int PAIR>
+// SPEC: the speculative stack pop (kFlagSpecPop) compiled in.  A separate
+// instantiation, not only a runtime flag: its code in the hot loop costs the
+// low-load (<= 2 sources per CU) kernel ~8 us at k=48 even when the flag is
+// off (144 sources 44.3 vs 52.0 us, same box, gpurun_out/r5_abr4), while at
+// the headline's load the pop itself gains
+template <int NW, bool HOPS, bool PACKED, bool C16, int PAIR, bool SPEC = false>
 __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
     int V, const uint16_t *__restrict__ adj, const uint16_t *__restrict__ radj,
     const uint32_t *__restrict__ deg, const int32_t *__restrict__ row_ptr,
@@ -1815,7 +1820,7 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                     below = __popcll(mm & ((1ull << hl) - 1ull));   // fresh children under it
                     pu[0] = nu;
                     xp[0] = adj[(size_t)nu * 64 + lane];
-                } else if ((flags & kFlagSpecPop) && sp > 0) {
+                } else if (SPEC && (flags & kFlagSpecPop) && sp > 0) {
                     // every fresh child is a leaf (its count is 0 and counts
                     // never rise), so none stays on the stack and the next
                     // candidate is the first entry with a count from the top
@@ -2549,6 +2554,18 @@ static bool dfs_bits_default(const char *force)
 
 #endif
 
+// the async kernel for a row form: compact LDS (C16), paired in-rows,
+// dword-paired in-rows, or plain u16 in-rows
+template <int N_, bool H_, bool P_, bool SPEC>
+static auto async_pick(bool c16, bool pair, bool dw)
+{
+    return c16 ? (pair ? dfs_async_kernel<N_, H_, P_, true, 1, SPEC>
+                       : dfs_async_kernel<N_, H_, P_, true, 0, SPEC>)
+               : (pair ? dfs_async_kernel<N_, H_, P_, false, 1, SPEC>
+                       : (dw ? dfs_async_kernel<N_, H_, P_, false, 2, SPEC>
+                             : dfs_async_kernel<N_, H_, P_, false, 0, SPEC>));
+}
+
 // hop counts as u16 (0xFFFF unreached) into d_hops
 __global__ __launch_bounds__(256) void dfs_hops16_kernel(size_t n, const int32_t *__restrict__ h,
                                                          uint16_t *__restrict__ out)
@@ -2694,8 +2711,12 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         // runs (gpurun_out/r5_k): k=48 1,152 sources 90.8 / 91.2 -> 90.4 /
         // 90.5 us, 144 sources 56.4 -> 55.5 us, one source 53.7 -> 53.4 us,
         // dragonfly 195.8 -> 192.9 us
+        // Compiled into the 3- and 4-wave kernels only (the loaded regimes,
+        // > 2 sources per CU): its code cost the 8-wave low-load kernel ~8 us
+        // even switched off (see dfs_async_kernel's SPEC)
         bool specpop = true;
         if (const char *f = getenv("SDNROUTE_DFS_SPECPOP")) specpop = !strcmp(f, "1");
+        const bool spec = specpop;
         const int aflags = dfs_flags(kFlagPrio) | (preswz ? kFlagPreSwz : 0) | hflags |
                            (specpop ? kFlagSpecPop : 0);
         // paired worker rows (in-degree <= 32, pre-swizzled rows only);
@@ -2717,11 +2738,9 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         ctx->last_kernel = names[nw];
 #define SDNR_ASYNC_P(N_, H_, P_)                                                             \
     do {                                                                                     \
-        auto k = c16 ? (pair ? dfs_async_kernel<N_, H_, P_, true, 1>                         \
-                             : dfs_async_kernel<N_, H_, P_, true, 0>)                        \
-                     : (pair ? dfs_async_kernel<N_, H_, P_, false, 1>                        \
-                             : (dw ? dfs_async_kernel<N_, H_, P_, false, 2>                  \
-                                   : dfs_async_kernel<N_, H_, P_, false, 0>));               \
+        constexpr bool kSpecOk = N_ == 3 || N_ == 4;   /* the loaded regimes */              \
+        auto k = spec && kSpecOk ? async_pick<N_, H_, P_, kSpecOk>(c16, pair, dw)            \
+                                 : async_pick<N_, H_, P_, false>(c16, pair, dw);             \
         allow_full_lds(k);                                                                   \
         hipLaunchKernelGGL(k, dim3(cgrid), dim3(N_ * 64), cl, ctx->stream, V, ctx->adj16,    \
                            preswz ? rw : ctx->radj16, ctx->deg32, ctx->row_ptr,              \
