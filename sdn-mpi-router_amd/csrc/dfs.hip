@@ -2559,10 +2559,13 @@ static bool dfs_bits_default(const char *force)
 template <int N_, bool H_, bool P_, bool SPEC>
 static auto async_pick(bool c16, bool pair, bool dw)
 {
-    return c16 ? (pair ? dfs_async_kernel<N_, H_, P_, true, 1, SPEC>
-                       : dfs_async_kernel<N_, H_, P_, true, 0, SPEC>)
-               : (pair ? dfs_async_kernel<N_, H_, P_, false, 1, SPEC>
-                       : (dw ? dfs_async_kernel<N_, H_, P_, false, 2, SPEC>
+    // (SPEC: the plain-row kernel only -- the compact / paired forms, the
+    // dragonfly's, measured slower with the speculative pop compiled in:
+    // 2,064 sources 177.3 -> 180.4 us, gpurun_out/r5_abspec)
+    return c16 ? (pair ? dfs_async_kernel<N_, H_, P_, true, 1>
+                       : dfs_async_kernel<N_, H_, P_, true, 0>)
+               : (pair ? dfs_async_kernel<N_, H_, P_, false, 1>
+                       : (dw ? dfs_async_kernel<N_, H_, P_, false, 2>
                              : dfs_async_kernel<N_, H_, P_, false, 0, SPEC>));
 }
 
@@ -2707,13 +2710,12 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         const char *pz = getenv("SDNROUTE_DFS_PRESWZ");
         const uint16_t *rw = c16 ? ctx->radjc : ctx->radjw;
         const bool preswz = rw && !(pz && !strcmp(pz, "0"));
-        // speculative stack pops (SDNROUTE_DFS_SPECPOP=0|1), same box, two
-        // runs (gpurun_out/r5_k): k=48 1,152 sources 90.8 / 91.2 -> 90.4 /
-        // 90.5 us, 144 sources 56.4 -> 55.5 us, one source 53.7 -> 53.4 us,
-        // dragonfly 195.8 -> 192.9 us
-        // Compiled into the 3- and 4-wave kernels only (the loaded regimes,
-        // > 2 sources per CU): its code cost the 8-wave low-load kernel ~8 us
-        // even switched off (see dfs_async_kernel's SPEC)
+        // speculative stack pops (SDNROUTE_DFS_SPECPOP=0|1).
+        // Compiled into the 4-wave plain-row kernel only (the k=48
+        // headline's regime: 1,152 sources 83.0 -> 82.3 us, same ISA with
+        // the pop off / on): its code cost the 8-wave low-load kernel ~8 us
+        // even switched off, and the dragonfly's 3-wave compact kernel 1-2 %
+        // (see dfs_async_kernel's SPEC; gpurun_out/r5_abr4, r5_abspec)
         bool specpop = true;
         if (const char *f = getenv("SDNROUTE_DFS_SPECPOP")) specpop = !strcmp(f, "1");
         const bool spec = specpop;
@@ -2738,7 +2740,7 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         ctx->last_kernel = names[nw];
 #define SDNR_ASYNC_P(N_, H_, P_)                                                             \
     do {                                                                                     \
-        constexpr bool kSpecOk = N_ == 3 || N_ == 4;   /* the loaded regimes */              \
+        constexpr bool kSpecOk = N_ == 4;              /* the k=48 headline's regime */      \
         auto k = spec && kSpecOk ? async_pick<N_, H_, P_, kSpecOk>(c16, pair, dw)            \
                                  : async_pick<N_, H_, P_, false>(c16, pair, dw);             \
         allow_full_lds(k);                                                                   \
