@@ -15,9 +15,12 @@ when no launcher did): the sources are split into contiguous blocks, each
 rank builds its block, and the blocks are assembled over RCCL -- by default
 on rank 0, the controller's GPU (point-to-point receives, SURVEY.md 8(e)'s
 "or on GPU 0 only"), with ``--assemble all`` by an all-gather onto every
-rank; the other form is timed beside it.  Consecutive steps may be kept in
-flight on their own streams (``--inflight``) so that a rank's share fills
-its GPU.  Fixed total work per step -> "scaling": "strong".
+rank; the other form is timed beside it.  At N > 1 three consecutive steps
+are kept in flight on their own streams (``--inflight``) so that a rank's
+share fills its GPU; the N = 1 line runs one step at a time (its roofline is
+per launch) and reports the same GPU with 3 steps in flight as
+``pipelined``, the like-for-like base for an N > 1 line.  Fixed total work
+per step -> "scaling": "strong".
 
 The JSON line also carries
   roofline      algorithmic bytes of the DFS kernel per launch
@@ -88,10 +91,10 @@ def parse():
                          "rank (RCCL all-gather); the other form is measured beside it in "
                          "the multi_gpu block")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="N > 1: steps kept in flight on their own streams (0: auto -- as "
-                         "many as it takes for one rank's share of the sources to fill its "
-                         "GPU, at most 3; 1 at N = 1).  Every step still computes and "
-                         "assembles all tables")
+                    help="steps kept in flight on their own streams (0: auto -- 3 at N > 1, "
+                         "where one rank's share leaves most of its GPU idle; 1 at N = 1, "
+                         "whose line then also reports the same GPU with 3 in flight as "
+                         "'pipelined').  Every step still computes and assembles all tables")
     ap.add_argument("--rehearse", action="store_true",
                     help="launcher rehearsal on CPU: the N ranks form a gloo group, shard "
                          "the sources and assemble them, and rank 0 prints the line's "
@@ -822,6 +825,49 @@ def main_rehearse(args, world, rank):
     return 0 if ok else 1
 
 
+def pipelined_rate(local, dev, csr, t_src, per, tables, slots, packed, mode, routes, steps,
+                   k=3):
+    """The same step with k consecutive steps in flight on their own streams
+    and library contexts (what an N > 1 rank runs), one GPU: every step
+    still computes every table of the step."""
+    streams = [torch.cuda.Stream(dev) for _ in range(k)]
+    ctxs = []
+    for st in streams:
+        c = _native.Context(local)
+        c.upload(csr)
+        c.set_stream(st.cuda_stream)
+        ctxs.append(c)
+    bufs = [tables() for _ in range(k)]
+
+    def launch(i):
+        c, tb = ctxs[i % k], bufs[i % k]
+        with torch.cuda.stream(streams[i % k]):
+            if slots:
+                c.dfs_tables_slots_device(t_src.data_ptr(), per, tb[0].data_ptr())
+            elif packed:
+                c.dfs_tables_packed_device(t_src.data_ptr(), per, tb[0].data_ptr())
+            elif mode == "dfs":
+                c.dfs_tables_device(t_src.data_ptr(), per, tb[0].data_ptr(), tb[1].data_ptr())
+            else:
+                c.shortest_tables_device(t_src.data_ptr(), per, tb[0].data_ptr(),
+                                         tb[1].data_ptr(), tb[2].data_ptr())
+    for i in range(2 * k):
+        launch(i)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        launch(i)
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    for c in ctxs:
+        c.synchronize()
+        c.close()
+    return {"steps_in_flight": k, "ms_per_step": ms, "value": routes / (ms / 1e3),
+            "steps": steps,
+            "note": "same workload, %d consecutive steps in flight on their own streams (as "
+                    "an N > 1 rank runs them); every step computes every table" % k}
+
+
 def main():
     args = parse()
     env_world = os.environ.get("WORLD_SIZE")
@@ -919,9 +965,14 @@ def main():
     # tables -- run on their own streams so that a rank keeps about as many
     # sources resident as one GPU holds at N = 1 (4 per CU); two table sets
     # per stream, so a step's kernel overlaps the previous step's gather
-    cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    inflight = args.inflight if args.inflight > 0 else \
-        (1 if world == 1 else max(1, min(3, -(-4 * cus // max(1, per)))))
+    # (3 in flight is the most that pays: HIP gives a process 4 hardware
+    # queues, and RCCL's stream takes one; one GPU, k=48 shares of 144 / 288 /
+    # 576 sources: 47.5 -> 20.9 / 26.5 / 39.2 us per step at 3, 28.4 / 34.0
+    # at 4, profiles/r05_inflight_sweep.jsonl).  N = 1 keeps one step at a
+    # time -- the line's per-launch roofline -- and reports the same GPU's
+    # rate with 3 in flight beside it ("pipelined"), the like-for-like base
+    # of an N > 1 line
+    inflight = args.inflight if args.inflight > 0 else (1 if world == 1 else 3)
     streams = [stream] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
     # one library context per stream in flight: a context's scratch (the split
     # kernel's spill rings and chunk cursors, the watchdog word) serves one
@@ -1005,6 +1056,10 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     routes = float(counts.sum()) * float(H)      # every host pair of these sources
     value = routes / (ms_per_step / 1e3)
+    pipelined = None
+    if world == 1 and inflight == 1 and args.inflight == 0:
+        pipelined = pipelined_rate(local, dev, csr, t_src, per, tables, slots, packed,
+                                   args.mode, routes, max(args.steps, 30))
     multi = None
     if world > 1:
         multi = multi_gpu_extras(args, world, rank, local, dev, csr, srcs, per, packed, slots,
@@ -1070,6 +1125,8 @@ def main():
         "switch_pair_routes_per_s": float(S) * V / (ms_per_step / 1e3),
         "teps": float(hi - lo) * E / (kern_ms / 1e3),
     }
+    if pipelined is not None:
+        out["pipelined"] = pipelined
     if multi is not None:
         multi["process_group"] = {"backend": dist.get_backend(),
                                   "world_size": dist.get_world_size()}
