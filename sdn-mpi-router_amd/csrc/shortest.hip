@@ -1293,7 +1293,16 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
     if (apsp_ok && (!strcmp(force, "apsp") || (!*force && sp_apsp_default(ctx, ndst))))
         return launch_sp_apsp(ctx, d_dst, ndst, d_dist, d_nh, d_nh_port);
     const bool plane_ok = ctx->W > 0 && ctx->W <= 64;
-    const bool plane_big = (size_t)ndst * (size_t)V >= ((size_t)1 << 21);
+    // ... and on any batch of a graph of >= 1,024 vertices, where one
+    // workgroup walking a destination's whole BFS is slower than the plane
+    // BFS's level launches even for a single destination (back-to-back, one
+    // box, gpurun_out/r5_absp2/3: k=48 1 / 144 / 576 destinations 123.6 /
+    // 125.6 / 150.1 -> 70.2 / 74.8 / 77.3 us -- the N = 8 / N = 2 shares of
+    // an all-pairs step were slower than the whole 1,152 (84.8 us); dragonfly
+    // a16 h8 144 destinations 88.9 -> 42.6 us; fat-tree k=32 (V = 1,280) 61
+    // -> 53 us; below, k=24 (V = 720) 40 vs 46 us and k=8 14 vs 38 us keep
+    // the per-destination kernel)
+    const bool plane_big = (size_t)ndst * (size_t)V >= ((size_t)1 << 21) || V >= 1024;
     if (plane_ok && (!strcmp(force, "plane") || (!*force && plane_big))) {
         const int rc = launch_plane(ctx, d_dst, ndst, d_dist, d_nh, d_nh_port);
         if (rc <= 0) return rc;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B of the k=48 packed DFS tables between library builds (diagnostic).
 
-    python tools/ab_lib_dfs.py [--fabric NAME] LIB[:ENV=VALUE] ...
+    python tools/ab_lib_dfs.py [--fabric NAME] [--shortest] LIB[:ENV=VALUE] ...
 
 Each library is loaded through plain ctypes (no build-identity check, so an
 older build of the product library works too), the k=48 CSR uploaded, and
@@ -26,6 +26,7 @@ def open_lib(path):
     L.sdnr_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.sdnr_graph_upload.argtypes = [vp, i32, i32, vp, vp, vp]
     L.sdnr_dfs_tables_packed.argtypes = [vp, vp, i32, vp, u32]
+    L.sdnr_shortest_tables.argtypes = [vp, vp, i32, vp, vp, vp, u32]
     L.sdnr_set_stream.argtypes = [vp, vp]
     L.sdnr_synchronize.argtypes = [vp]
     h = vp()
@@ -38,6 +39,9 @@ def main():
     fab = "fat_tree:48"
     if args and args[0] == "--fabric":
         fab, args = args[1], args[2:]
+    shortest = bool(args) and args[0] == "--shortest"
+    if shortest:
+        args = args[1:]
     specs = [(a.split(":", 1) + [""])[:2] for a in args]    # (library, "ENV=VALUE" or "")
     libs = [a for a in args]
     fabric = T.by_name(fab)
@@ -59,11 +63,12 @@ def main():
         L.sdnr_set_stream(h, ctypes.c_void_p(stream.cuda_stream))
         opened.append((p, L, h, env))
     res = {p: {} for p in libs}
-    ns = [n for n in (1, 144, 1152, len(srcs)) if n <= len(srcs)]
+    ns = [n for n in (1, 8, 32, 144, 258, 288, 516, 576, 1152, len(srcs)) if n <= len(srcs)]
     for n in sorted(set(ns)):
         pick = srcs[np.linspace(0, len(srcs) - 1, n).astype(np.int64)]
         ts = torch.from_numpy(pick).to(dev)
         out = torch.empty((n, csr.V), dtype=torch.int32, device=dev)
+        o2, o3 = torch.empty_like(out), torch.empty_like(out)
         torch.cuda.synchronize(dev)
         for rep in range(6):
             for p, L, h, env in opened:
@@ -73,7 +78,12 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
                 for _ in range(10):
-                    assert L.sdnr_dfs_tables_packed(h, ts.data_ptr(), n, out.data_ptr(), 1) == 0
+                    if shortest:
+                        assert L.sdnr_shortest_tables(h, ts.data_ptr(), n, out.data_ptr(),
+                                                      o2.data_ptr(), o3.data_ptr(), 1) == 0
+                    else:
+                        assert L.sdnr_dfs_tables_packed(h, ts.data_ptr(), n, out.data_ptr(),
+                                                        1) == 0
                 e1.record(stream)
                 torch.cuda.synchronize(dev)
                 assert L.sdnr_synchronize(h) == 0
@@ -82,7 +92,7 @@ def main():
                 if rep:
                     res[p].setdefault(n, []).append(e0.elapsed_time(e1) / 10 * 1e3)
     for p in libs:
-        print(fab, os.path.basename(p), {n: round(float(np.median(v)), 1) for n, v in res[p].items()})
+        print(fab, "shortest" if shortest else "dfs", os.path.basename(p), {n: round(float(np.median(v)), 1) for n, v in res[p].items()})
 
 
 if __name__ == "__main__":
