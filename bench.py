@@ -57,7 +57,9 @@ TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    # 100 steps: the timed region's fixed cost (barrier, synchronisation,
+    # the first launch's latency; ~0.1 ms) was 5 % of a 20-step k=48 run
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--fabric", default="fat_tree:48")
     ap.add_argument("--mode", choices=["dfs", "shortest", "flows", "ecmp", "apsp", "matflows"],
@@ -77,7 +79,7 @@ def parse():
                     help="dfs/shortest: every switch as a source/destination (V x V switch "
                          "pairs, e.g. route_tables('shortest', vertices=all)) instead of the "
                          "host-bearing ones; value counts switch pairs")
-    ap.add_argument("--event-every", type=int, default=4,
+    ap.add_argument("--event-every", type=int, default=10,
                     help="bracket every k-th timed launch with HIP events (kernel time; "
                          "the events themselves cost a few us per step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
