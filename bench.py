@@ -16,8 +16,8 @@ rank builds its block, and the blocks are assembled over RCCL -- by default
 on rank 0, the controller's GPU (point-to-point receives, SURVEY.md 8(e)'s
 "or on GPU 0 only"), with ``--assemble all`` by an all-gather onto every
 rank; the other form is timed beside it.  At N > 1 three consecutive steps
-are kept in flight on their own streams (``--inflight``) so that a rank's
-share fills its GPU; the N = 1 line runs one step at a time (its roofline is
+are kept in flight on their own streams (``--inflight``) when a rank's share
+is under 4 sources per CU (k=48), so that it fills its GPU; the N = 1 line runs one step at a time (its roofline is
 per launch) and reports the same GPU with 3 steps in flight as
 ``pipelined``, the like-for-like base for an N > 1 line.  Fixed total work
 per step -> "scaling": "strong".
@@ -93,8 +93,9 @@ def parse():
                          "rank (RCCL all-gather); the other form is measured beside it in "
                          "the multi_gpu block")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="steps kept in flight on their own streams (0: auto -- 3 at N > 1, "
-                         "where one rank's share leaves most of its GPU idle; 1 at N = 1, "
+                    help="steps kept in flight on their own streams (0: auto -- 3 at N > 1 "
+                         "when one rank's share is under 4 sources per CU and leaves most of "
+                         "its GPU idle (k=48), else 1; 1 at N = 1, "
                          "whose line then also reports the same GPU with 3 in flight as "
                          "'pipelined').  Every step still computes and assembles all tables")
     ap.add_argument("--rehearse", action="store_true",
@@ -974,7 +975,11 @@ def main():
     # time -- the line's per-launch roofline -- and reports the same GPU's
     # rate with 3 in flight beside it ("pipelined"), the like-for-like base
     # of an N > 1 line
-    inflight = args.inflight if args.inflight > 0 else (1 if world == 1 else 3)
+    # (a share of >= 4 sources per CU -- the torus, Jellyfish -- fills the GPU
+    # with one step, and its table sets are large: one step at a time)
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    inflight = args.inflight if args.inflight > 0 else \
+        (3 if world > 1 and per < 4 * cus else 1)
     streams = [stream] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
     # one library context per stream in flight: a context's scratch (the split
     # kernel's spill rings and chunk cursors, the watchdog word) serves one
@@ -1059,7 +1064,9 @@ def main():
     routes = float(counts.sum()) * float(H)      # every host pair of these sources
     value = routes / (ms_per_step / 1e3)
     pipelined = None
-    if world == 1 and inflight == 1 and args.inflight == 0:
+    set_bytes = sum(t.numel() * t.element_size() for t in bufs[0])
+    if world == 1 and inflight == 1 and args.inflight == 0 and 3 * set_bytes <= (4 << 30) \
+            and ms_per_step <= 10.0:      # small steps only: 3 more table sets, 30+ steps
         pipelined = pipelined_rate(local, dev, csr, t_src, per, tables, slots, packed,
                                    args.mode, routes, max(args.steps, 30))
     multi = None

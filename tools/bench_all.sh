@@ -9,14 +9,14 @@ run() {  # fabric mode steps warmup extra...
 run mock dfs 50 5
 run fat_tree:8 dfs 50 5
 run fat_tree:8 shortest 50 5 --no-cpu-baseline
-run fat_tree:48 dfs 20 3
-run fat_tree:48 dfs 20 3 --layout int32 --no-cpu-baseline
-run fat_tree:48 shortest 10 2 --no-cpu-baseline
+run fat_tree:48 dfs 100 3
+run fat_tree:48 dfs 100 3 --layout int32 --no-cpu-baseline
+run fat_tree:48 shortest 50 2 --no-cpu-baseline
 run fat_tree:48 flows 10 2 --ranks 1024
 run fat_tree:48 ecmp 10 2
 run fat_tree:48 apsp 5 1
-run dragonfly:16,8,8 dfs 10 2
-run dragonfly:16,8,8 shortest 5 1 --no-cpu-baseline
+run dragonfly:16,8,8 dfs 50 2
+run dragonfly:16,8,8 shortest 20 1 --no-cpu-baseline
 TMO=600 run torus:32,32,32 dfs 2 1 --cpu-budget-s 8
 TMO=600 run torus:32,32,32 shortest 2 1 --no-cpu-baseline
 TMO=900 run jellyfish:100000,16,1 dfs 2 1 --cpu-budget-s 8
