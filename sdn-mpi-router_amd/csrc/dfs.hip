@@ -2513,7 +2513,16 @@ static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, in
         if (hops) SDNR_SPLIT_F(L_, J_, R_, true); else SDNR_SPLIT_F(L_, J_, R_, false);      \
     } while (0)
     if constexpr (kWide) {
+        // stack entries per window: 8 (J = 2; SDNROUTE_DFS_SPLIT_J=4|1 for 16 |
+        // 4).  Same box, 100k Jellyfish, all sources (gpurun_out/r5_jfj2): 16
+        // entries 880 ms, 8 entries 833 ms, 4 entries 875 ms -- the window's
+        // row loads (the CU's data return is ~90 % busy) against the leaf
+        // skips a narrower window takes more iterations for
+        const char *jf = getenv("SDNROUTE_DFS_SPLIT_J");
+        const int jw = jf && (atoi(jf) == 4 || atoi(jf) == 1) ? atoi(jf) : 2;
         if (ring == 256) SDNR_SPLIT_H(16, 4, 256);
+        else if (jw == 2) SDNR_SPLIT_H(16, 2, 512);
+        else if (jw == 1) SDNR_SPLIT_H(16, 1, 512);
         else SDNR_SPLIT_H(16, 4, 512);
     } else {
         if (lpr == 8 && ring == 128) SDNR_SPLIT_H(8, 1, 128);

@@ -306,12 +306,14 @@ def test_dfs_fullsize_all_host_sources(ctx, name):
 
 
 @pytest.mark.parametrize("split", ["1", "0", "ns3", "ns7", "ns5", "ns5-ring256", "ns11-ring256",
-                                   "cumap0", "cumap1"])
+                                   "cumap0", "cumap1", "j4", "j1"])
 @pytest.mark.parametrize("name,nsample", [("torus_32x32x32_sample", 384),
                                           ("jellyfish_n100000_r16_sample", 48)])
 def test_dfs_fullsize_sampled_sources(ctx, monkeypatch, name, nsample, split):
     if split.startswith("cumap"):                # sources by CU chunk or strided
         monkeypatch.setenv("SDNROUTE_DFS_CUMAP", split[-1])
+    elif split.startswith("j"):                  # stack entries per window (rows of 9-16 slots)
+        monkeypatch.setenv("SDNROUTE_DFS_SPLIT_J", split[1:])
     elif split.startswith("ns"):                 # search waves per workgroup
         ns, _, ring = split[2:].partition("-ring")
         monkeypatch.setenv("SDNROUTE_DFS_SPLIT_NS", ns)
