@@ -1626,10 +1626,18 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
 #ifndef SDNR_ASYNC_G_P1
 #define SDNR_ASYNC_G_P1 8
 #endif
+#ifndef SDNR_ASYNC_G_U16
+#define SDNR_ASYNC_G_U16 32
+#endif
     // children per worker step: 16 (8 above 4 waves), and 16 with the
     // dword-paired rows of the 5-worker regime (8 loads): k=48 144 sources
     // 54.9 -> 48.8 us, one source 53.3 -> 47.2 us (fresher counts)
-    constexpr int G = NW <= 4 ? SDNR_ASYNC_G
+    // Round 5: 32 with the plain u16 in-rows at <= 4 waves (the k=48
+    // headline; library A/B, one box, gpurun_out/r5_abg3: 1,152 sources
+    // 82.5 / 80.6 / 79.4 / 78.8 / 85.1 us at 16 / 24 / 32 / 48 / 64, 576
+    // sources 67.4 -> 64.9 at 32), while the dragonfly's paired rows keep 16
+    // (2,064 sources 185.6 -> 214.1 us at 32)
+    constexpr int G = NW <= 4 ? (PAIR == 0 ? SDNR_ASYNC_G_U16 : SDNR_ASYNC_G)
                               : (PAIR == 2 ? SDNR_ASYNC_G_DW : (PAIR == 1 ? SDNR_ASYNC_G_P1 : 8));
     constexpr unsigned kSpin = 1u << 22;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];

@@ -35,6 +35,7 @@ def open_lib(path):
 
 
 def main():
+    print("torch imported", file=sys.stderr, flush=True)
     args = sys.argv[1:]
     fab = "fat_tree:48"
     if args and args[0] == "--fabric":
@@ -62,8 +63,12 @@ def main():
                                    port.ctypes.data) == 0
         L.sdnr_set_stream(h, ctypes.c_void_p(stream.cuda_stream))
         opened.append((p, L, h, env))
+        print("opened %s" % p, file=sys.stderr, flush=True)
     res = {p: {} for p in libs}
+    only = os.environ.get("AB_NS")            # e.g. "144,1152": these counts only
     ns = [n for n in (1, 8, 32, 144, 258, 288, 516, 576, 1152, len(srcs)) if n <= len(srcs)]
+    if only:
+        ns = [n for n in ns if str(n) in only.split(",") or (n == len(srcs) and "all" in only)]
     for n in sorted(set(ns)):
         pick = srcs[np.linspace(0, len(srcs) - 1, n).astype(np.int64)]
         ts = torch.from_numpy(pick).to(dev)
@@ -91,6 +96,7 @@ def main():
                     del os.environ[k]
                 if rep:
                     res[p].setdefault(n, []).append(e0.elapsed_time(e1) / 10 * 1e3)
+        print("done n=%d" % n, file=sys.stderr, flush=True)      # progress (a silent run looks hung)
     for p in libs:
         print(fab, "shortest" if shortest else "dfs", os.path.basename(p), {n: round(float(np.median(v)), 1) for n, v in res[p].items()})
 

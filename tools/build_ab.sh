@@ -7,7 +7,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 C=$ROOT/sdn-mpi-router_amd/csrc
 OUT=$ROOT/tools/ab/$NAME; mkdir -p $OUT
 pids=()
-for f in capi dfs shortest apsp routes ecmp; do
+for f in capi dfs shortest apsp routes ecmp incremental; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function "$@" -c -o $OUT/$f.o $C/$f.hip &
   pids+=($!)
 done
