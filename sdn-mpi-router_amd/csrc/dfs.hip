@@ -1618,7 +1618,7 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
     constexpr int S = NW - 1;                    // workers
     constexpr int RING = 512;                    // children in flight (u16)
 #ifndef SDNR_ASYNC_G
-#define SDNR_ASYNC_G 16
+#define SDNR_ASYNC_G 8
 #endif
 #ifndef SDNR_ASYNC_G_DW
 #define SDNR_ASYNC_G_DW 16
@@ -1635,8 +1635,9 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
     // Round 5: 32 with the plain u16 in-rows at <= 4 waves (the k=48
     // headline; library A/B, one box, gpurun_out/r5_abg3: 1,152 sources
     // 82.5 / 80.6 / 79.4 / 78.8 / 85.1 us at 16 / 24 / 32 / 48 / 64, 576
-    // sources 67.4 -> 64.9 at 32), while the dragonfly's paired rows keep 16
-    // (2,064 sources 185.6 -> 214.1 us at 32)
+    // sources 67.4 -> 64.9 at 32), while the dragonfly's paired rows want
+    // narrower steps: 8 (2,064 sources 178.9 / 171.8 / 168.5 us at 16 / 12 /
+    // 8, 214.1 at 32; gpurun_out/r5_abg5)
     constexpr int G = NW <= 4 ? (PAIR == 0 ? SDNR_ASYNC_G_U16 : SDNR_ASYNC_G)
                               : (PAIR == 2 ? SDNR_ASYNC_G_DW : (PAIR == 1 ? SDNR_ASYNC_G_P1 : 8));
     constexpr unsigned kSpin = 1u << 22;
