@@ -748,6 +748,107 @@ __global__ __launch_bounds__(256) void msbfs_plane_init_kernel(
     }
 }
 
+// The init kernel with level 1 folded in.  Level 1
+// needs no frontier plane: vertex x is reached at level 1 by destination bit
+// b exactly when one of its out-neighbours IS destination b, and the bit takes
+// the first such slot (the level kernel's lexicographic rule).  So thread
+// (batch, x) computes the seed words of its row's neighbours from the batch's
+// destination list itself -- an index test when the batch is an ascending run
+// of ids (every benched destination set), else the 64-lane match -- and
+// writes the planes as they stand after level 1: visited = seed | new,
+// frontier = seed, next = new, level plane 0 = new, slot planes.  The level
+// flags and complete-word counters must be zero before it runs (the host
+// clears them: this kernel's blocks add into them), and the host starts the
+// level sequence at 2.
+template <int SB, int DP>
+__global__ __launch_bounds__(256) void msbfs_plane_init1_kernel(
+    int V, int VS, int W, const int32_t *__restrict__ ell_col, const int32_t *__restrict__ dst,
+    int ndst, uint64_t *__restrict__ pl, int *__restrict__ flags, int *__restrict__ status)
+{
+    constexpr int NPL = plane_count_dp(SB, DP);
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int batch = blockIdx.y;
+    const int nb = min(64, ndst - batch * 64);
+    const uint64_t all = nb == 64 ? ~0ull : ((1ull << nb) - 1ull);
+    const int lane = lane_id();
+    const int mine = lane < nb ? dst[batch * 64 + lane] : -1;
+    int lo = (lane < nb && mine >= 0 && mine < V) ? mine : 0x7FFFFFFF;
+    int hi = lane < nb ? mine : -1;
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, __shfl_xor(lo, o));
+        hi = max(hi, __shfl_xor(hi, o));
+    }
+    // an ascending run lo, lo + 1, ..., lo + nb - 1 of valid ids
+    const bool run = __ballot(lane < nb && mine != lo + lane) == 0ull && lo + nb <= V;
+    auto seed_of = [&](int v) -> uint64_t {
+        if (v < lo || v > hi || v >= V) return 0ull;
+        if (run) return 1ull << (v - lo);
+        uint64_t s = 0ull;
+        for (int k = 0; k < nb; ++k)
+            if (__builtin_amdgcn_readlane(mine, k) == v) s |= 1ull << k;
+        return s;
+    };
+    uint64_t seed = 0ull, nw = 0ull, rem = 0ull, sp[SB];
+#pragma unroll
+    for (int k = 0; k < SB; ++k) sp[k] = 0ull;
+    if (x < V) {
+        seed = seed_of(x);
+        if ((seed & all) != all) {
+            constexpr int WM = 1 << SB;
+            const int32_t *r = ell_col + (size_t)x * W;
+            int n[WM];
+#pragma unroll
+            for (int j = 0; j < WM; ++j) n[j] = j < W ? r[j] : -1;
+            rem = ~seed & all;
+#pragma unroll
+            for (int j = 0; j < WM; ++j) {
+                if (j < W && n[j] >= 0) {
+                    const uint64_t h = seed_of(n[j]) & rem;
+                    rem &= ~h;
+#pragma unroll
+                    for (int k = 0; k < SB; ++k)
+                        if ((j >> k) & 1) sp[k] |= h;
+                }
+            }
+            nw = (~seed & all) & ~rem;
+        }
+    }
+    if (x < VS) {
+        uint64_t *b = pl + (size_t)batch * NPL * VS + x;
+#pragma unroll
+        for (int p = 0; p < NPL; ++p) {
+            uint64_t w = 0ull;
+            if (p == kPlVis) w = seed | nw;
+            else if (p == kPlFront) w = seed;
+            else if (p == kPlNext || p == kPlDist) w = nw;
+            else if (p >= kPlDist + DP && p < kPlDist + DP + SB) w = sp[p - kPlDist - DP];
+            b[(size_t)p * VS] = w;
+        }
+    }
+    {
+        const uint64_t act = __ballot(true);
+        const uint64_t fm = __ballot(nw != 0ull && rem == 0ull), am = __ballot(nw != 0ull);
+        if (lane == __builtin_ctzll(act)) {
+            if (fm) atomicAdd(&status[16 * (blockIdx.x & 15)], __popcll(fm));
+            if (am && flags[1] == 0) flags[1] = 1;   // racing writers all store 1
+        }
+    }
+    if (batch == 0 && blockIdx.x == 0) {
+        // words complete from the start (a batch of one repeated valid
+        // destination), as msbfs_plane_init_kernel counts them
+        const int nbatch = (ndst + 63) >> 6;
+        int seeded = 0;
+        for (int bt = threadIdx.x; bt < nbatch; bt += blockDim.x) {
+            const int n0 = bt * 64, n1 = min(ndst, n0 + 64);
+            const int d = dst[n0];
+            bool same = d >= 0 && d < V;
+            for (int i = n0 + 1; same && i < n1; ++i) same = dst[i] == d;
+            seeded += same;
+        }
+        if (seeded) atomicAdd(&status[0], seeded);
+    }
+}
+
 // A busy level is a chain of dependent L2 round trips per thread -- visited
 // word, row, frontier gathers, then a read-modify-write of the level / slot
 // planes.  opt kPlAtomicOr: the plane updates are return-less atomic ORs
@@ -1137,6 +1238,10 @@ static int launch_plane_dp(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, ui
     // SDNROUTE_PLANE_INIT=0: fills + seed kernel instead of the init kernel
     const char *iq = getenv("SDNROUTE_PLANE_INIT");
     const bool oldinit = iq && !strcmp(iq, "0");
+    // level 1 folded into the init kernel (msbfs_plane_init1_kernel);
+    // SDNROUTE_PLANE_FUSE1=0 keeps the separate level-1 launch
+    const char *fq = getenv("SDNROUTE_PLANE_FUSE1");
+    const bool fuse1 = !oldinit && !(fq && !strcmp(fq, "0"));
     const size_t tl = d_nh ? (size_t)2 * W * 257 * sizeof(int32_t) : 0;   // kTabStride, TB 256
     if (sb == 5 && tl > 65536) {  // W = 32 with the padded stride
         sdnr_allow_lds(reinterpret_cast<const void *>(msbfs_plane_tables_kernel<5, 256, 1, 8>), tl);
@@ -1172,6 +1277,24 @@ static int launch_plane_dp(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, ui
             hipLaunchKernelGGL(msbfs_plane_seed_kernel, dim3((nd + 255) / 256), dim3(256), 0,
                                ctx->stream, V, VS, d_dst + (size_t)c0 * 64, nd, pl, npl,
                                status);
+        } else if (fuse1) {
+            SDNR_HIP(hipMemsetAsync(changed, 0, kFlagInts * sizeof(int), ctx->stream));
+#define SDNR_INIT1(SB_, DP_)                                                                  \
+    hipLaunchKernelGGL((msbfs_plane_init1_kernel<SB_, DP_>), dim3((VS + lb - 1) / lb, nbc),       \
+                       dim3(lb), 0, ctx->stream, V, VS, W, ctx->ell_col,                          \
+                       d_dst + (size_t)c0 * 64, nd, pl, changed, status)
+            if (compact) {
+                if (sb == 3) SDNR_INIT1(3, 3);
+                else if (sb == 4) SDNR_INIT1(4, 3);
+                else if (sb == 5) SDNR_INIT1(5, 3);
+                else SDNR_INIT1(6, 3);
+            } else {
+                if (sb == 3) SDNR_INIT1(3, 8);
+                else if (sb == 4) SDNR_INIT1(4, 8);
+                else if (sb == 5) SDNR_INIT1(5, 8);
+                else SDNR_INIT1(6, 8);
+            }
+#undef SDNR_INIT1
         } else {
             hipLaunchKernelGGL(msbfs_plane_init_kernel, dim3((VS + lb - 1) / lb, nbc), dim3(lb), 0,
                                ctx->stream, V, VS, d_dst + (size_t)c0 * 64, nd, pl, npl,
@@ -1183,10 +1306,13 @@ static int launch_plane_dp(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, ui
         int32_t *nhp = d_nh_port ? d_nh_port + (size_t)c0 * 64 * V : nullptr;
         constexpr int kGroup = 8;
         const long long target = (long long)V * nbc;
-        int lvl = 1, upto = 0;
+        int lvl = fuse1 ? 2 : 1, upto = 0;
         int st[2] = {0, 0};
-        for (;;) {
+        for (bool first = true;; first = false) {
             upto = lvl <= guess ? guess : lvl + kGroup - 1;
+            // level 1 done by the init: a BFS the previous call finished at
+            // level 1 goes straight to the table pass
+            if (fuse1 && first && guess == 1) upto = 1;
             if (upto > 255) upto = 255;
             if (compact && upto > 7) upto = 7;
             for (; lvl <= upto; ++lvl) {

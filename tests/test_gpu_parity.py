@@ -544,7 +544,7 @@ def test_shortest_plane_compact_levels(ctx, monkeypatch, dp):
         np.testing.assert_array_equal(nhp, nhpo)
 
 
-@pytest.mark.parametrize("init", ["init", "seed"])
+@pytest.mark.parametrize("init", ["init", "nofuse", "seed"])
 @pytest.mark.parametrize("dp", ["auto", "8"])
 def test_shortest_plane_repeated_destinations(ctx, monkeypatch, dp, init):
     """Batches whose destinations are all one vertex ([5, 5], a full batch of
@@ -557,6 +557,8 @@ def test_shortest_plane_repeated_destinations(ctx, monkeypatch, dp, init):
         monkeypatch.setenv("SDNROUTE_PLANE_DP", dp)
     if init == "seed":
         monkeypatch.setenv("SDNROUTE_PLANE_INIT", "0")
+    if init == "nofuse":
+        monkeypatch.setenv("SDNROUTE_PLANE_FUSE1", "0")
     import torch
     csr = T.fat_tree(8).csr()
     ctx.upload(csr)
@@ -582,6 +584,32 @@ def test_shortest_plane_repeated_destinations(ctx, monkeypatch, dp, init):
         np.testing.assert_array_equal(nh[ok], nho)
         np.testing.assert_array_equal(nhp[ok], nhpo)
         assert (dist[~ok] == 0xFFFF).all() and (nh[~ok] == -1).all()
+
+
+@pytest.mark.parametrize("fuse", ["1", "0"])
+@pytest.mark.parametrize("fabric", ["fat_tree:8", "dragonfly:4,2,2", "torus:4,4,4"])
+def test_shortest_plane_level1_fold(ctx, monkeypatch, fabric, fuse):
+    """Level 1 folded into the plane init (msbfs_plane_init1_kernel): batches
+    that are ascending id runs take the index test, others (shuffled,
+    descending, strided, a run with a gap, a short last batch) the 64-lane
+    match; both, and the separate level-1 launch, bit-exact vs the oracle."""
+    monkeypatch.setenv("SDNROUTE_SP_STRATEGY", "plane")
+    monkeypatch.setenv("SDNROUTE_PLANE_FUSE1", fuse)
+    csr = T.by_name(fabric).csr()
+    ctx.upload(csr)
+    V = csr.V
+    rng = np.random.default_rng(7)
+    runs = np.arange(V, dtype=np.int32)
+    for dsts in (runs, rng.permutation(V).astype(np.int32), runs[::-1].copy(),
+                 runs[::3].copy(), np.r_[runs[:10], runs[12:80]].astype(np.int32),
+                 runs[V // 2:V // 2 + 5].copy(), np.asarray([V - 1], np.int32)):
+        for _ in range(2):                     # the second call runs on the cached depth
+            dist, nh, nhp = ctx.shortest_tables(dsts)
+            assert ctx.last_kernel().startswith("msbfs_plane_level_kernel")
+            do, nho, nhpo = O.dest_tables(csr, dsts, nthreads=NTHREADS)
+            np.testing.assert_array_equal(dist, do)
+            np.testing.assert_array_equal(nh, nho)
+            np.testing.assert_array_equal(nhp, nhpo)
 
 
 @pytest.mark.parametrize("strategy", ["auto", "msbfs", "plane", "lanes"])
