@@ -1627,7 +1627,7 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
 #define SDNR_ASYNC_G_P1 8
 #endif
 #ifndef SDNR_ASYNC_G_U16
-#define SDNR_ASYNC_G_U16 32
+#define SDNR_ASYNC_G_U16 48
 #endif
     // children per worker step: 16 (8 above 4 waves), and 16 with the
     // dword-paired rows of the 5-worker regime (8 loads): k=48 144 sources
@@ -1637,7 +1637,9 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
     // 82.5 / 80.6 / 79.4 / 78.8 / 85.1 us at 16 / 24 / 32 / 48 / 64, 576
     // sources 67.4 -> 64.9 at 32), while the dragonfly's paired rows want
     // narrower steps: 8 (2,064 sources 178.9 / 171.8 / 168.5 us at 16 / 12 /
-    // 8, 214.1 at 32; gpurun_out/r5_abg5)
+    // 8, 214.1 at 32; gpurun_out/r5_abg5).  48 for the plain rows after a
+    // second A/B on the final library (profiles/r05_async_g48_ab.log): 1,152
+    // sources 79.5 -> 78.2 us, every smaller share within 0.3 us
     constexpr int G = NW <= 4 ? (PAIR == 0 ? SDNR_ASYNC_G_U16 : SDNR_ASYNC_G)
                               : (PAIR == 2 ? SDNR_ASYNC_G_DW : (PAIR == 1 ? SDNR_ASYNC_G_P1 : 8));
     constexpr unsigned kSpin = 1u << 22;

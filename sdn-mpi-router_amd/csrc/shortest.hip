@@ -779,7 +779,8 @@ __global__ __launch_bounds__(256) void msbfs_plane_init1_kernel(
         hi = max(hi, __shfl_xor(hi, o));
     }
     // an ascending run lo, lo + 1, ..., lo + nb - 1 of valid ids
-    const bool run = __ballot(lane < nb && mine != lo + lane) == 0ull && lo + nb <= V;
+    // (lo is wave-uniform: the ballot runs on every lane or on none)
+    const bool run = lo <= V - nb && __ballot(lane < nb && mine != lo + lane) == 0ull;
     auto seed_of = [&](int v) -> uint64_t {
         if (v < lo || v > hi || v >= V) return 0ull;
         if (run) return 1ull << (v - lo);
