@@ -668,7 +668,7 @@ def _max_min(x, dev):
 
 
 def multi_gpu_extras(args, world, rank, local, dev, csr, srcs, per, packed, slots, kern_ms,
-                     ms_per_step, routes, step, drain, bufs, gathered, assemble):
+                     ms_per_step, routes, step, drain, bufs, gathered, assemble, check=None):
     """N > 1: what the step time is made of, and the other assembly forms.
 
     kernel_ms_max / _min  the route kernel per rank (HIP events);
@@ -703,16 +703,25 @@ def multi_gpu_extras(args, world, rank, local, dev, csr, srcs, per, packed, slot
     kmax, kmin = _max_min(kern_ms, dev)
     gather_ms = timed(gather_only)
     other = "root" if args.assemble == "all" else "all"
-    assemble[0] = other
-    other_ms = timed(step)
-    assemble[0] = args.assemble
+    # the secondary form is reported, never fatal for the headline (a form
+    # that failed its preflight is not run at all)
+    try:
+        if check and check.get(other) != "ok":
+            raise RuntimeError("preflight: %s" % check.get(other))
+        assemble[0] = other
+        other_ms = timed(step)
+        other_res = {"ms_per_step": other_ms, "value": routes / (other_ms / 1e3)}
+    except Exception as e:   # noqa: BLE001
+        other_res = {"error": repr(e)[:200]}
+    finally:
+        assemble[0] = args.assemble
     hidden = kmax + gather_ms - ms_per_step
     res = {
         "kernel_ms_max": kmax, "kernel_ms_min": kmin, "gather_ms": gather_ms,
         "overlap": max(0.0, min(1.0, hidden / max(1e-9, min(kmax, gather_ms)))),
         "assemble_" + args.assemble: {"ms_per_step": ms_per_step,
                                       "value": routes / (ms_per_step / 1e3)},
-        "assemble_" + other: {"ms_per_step": other_ms, "value": routes / (other_ms / 1e3)},
+        "assemble_" + other: other_res,
     }
     # one process over all devices (the controller's own process, TopologyDB(
     # devices=[...])): rank 0 alone, the others wait at the barrier
@@ -755,6 +764,70 @@ def multi_gpu_extras(args, world, rank, local, dev, csr, srcs, per, packed, slot
     if sp is not None:
         res["single_process"] = sp
     return res
+
+
+# why the line's default assembly is what it is (printed in config)
+ASSEMBLE_REASON = {
+    "root": "tables assembled on rank 0, the controller's GPU (the one process that serves "
+            "find_route, reference sdnmpi/topology.py:138-142): each peer's rows go straight "
+            "into its slice of the root's table over its own xGMI link (RCCL point-to-point, "
+            "SURVEY.md 8(e) 'or on GPU 0 only'); the north_star's all-gather delivers 7/8 of "
+            "the tables into EVERY GPU, ~7x the xGMI bytes of what the controller consumes, "
+            "and is timed beside it (multi_gpu.assemble_all)",
+    "all": "tables assembled on every rank by one RCCL all-gather per table over xGMI (the "
+           "north_star's form); the root-only point-to-point form is timed beside it "
+           "(multi_gpu.assemble_root)",
+}
+
+
+def n1_base(args, rank, local, dev, csr, srcs, tables, slots, packed, routes, est_ms):
+    """The N = 1 base of an N > 1 line, measured in the same run: rank 0's GPU
+    alone computes the WHOLE workload (all sources), one step at a time and
+    -- where the table sets are small -- with 3 steps in flight, exactly as
+    the N = 1 line's value / 'pipelined' do.  The other ranks wait at a
+    barrier.  Returns None on the other ranks."""
+    res = None
+    if rank == 0:
+        S = len(srcs)
+        t_all = torch.from_numpy(np.ascontiguousarray(srcs, np.int32)).to(dev)
+        set_bytes = sum(t.numel() * t.element_size() for t in tables(1)) * S
+        res = {"measured_on": "rank 0's GPU alone, all %d sources per step" % S}
+        try:
+            if set_bytes <= (48 << 30):
+                reps = int(max(2, min(max(args.steps, 30), 3000.0 / max(est_ms, 1e-3))))
+                res["inflight_1"] = pipelined_rate(local, dev, csr, t_all, S, lambda: tables(S),
+                                                   slots, packed, args.mode, routes, reps, k=1)
+            if 3 * set_bytes <= (4 << 30) and est_ms <= 10.0:
+                res["inflight_3"] = pipelined_rate(local, dev, csr, t_all, S, lambda: tables(S),
+                                                   slots, packed, args.mode, routes,
+                                                   max(args.steps, 30), k=3)
+        except Exception as e:   # noqa: BLE001 -- reported, not fatal for the headline
+            res["error"] = repr(e)[:200]
+        torch.cuda.synchronize(dev)
+    dist.barrier()
+    return res
+
+
+def scaling_keys(value, by_inflight, base, world):
+    """Scaling efficiency of an N > 1 line against its own run's N = 1 base:
+    like-for-like (same steps in flight as the headline when the base has
+    them) and one step at a time on both sides."""
+    if not base:
+        return {}
+    out = {}
+    head = next(v for v in by_inflight.values() if v.get("headline"))
+    k = head["steps_in_flight"]
+    b = base.get("inflight_%d" % k) or base.get("inflight_1")
+    if b:
+        out["scaling_efficiency"] = value / (world * b["value"])
+        out["scaling_efficiency_base"] = "n1_base.inflight_%d" % b["steps_in_flight"]
+    b1, h1 = base.get("inflight_1"), by_inflight.get("1")
+    if b1 and h1:
+        out["scaling_efficiency_one_at_a_time"] = h1["value"] / (world * b1["value"])
+    best = max([v["value"] for k_, v in base.items() if k_.startswith("inflight_")] or [0.0])
+    if best:
+        out["speedup_vs_n1_best"] = value / best
+    return out
 
 
 def _free_port():
@@ -801,27 +874,63 @@ def main_rehearse(args, world, rank):
     dist.init_process_group("gloo")
     fabric = T.by_name(args.fabric)
     hv, _ = fabric.host_table()
-    srcs = np.unique(hv).astype(np.int32)
+    srcs, counts = np.unique(hv, return_counts=True)
+    srcs = srcs.astype(np.int32)
     lo, hi, per = D.shard_bounds(len(srcs), world, rank)
+    check = D.check_assembly()              # the line's preflight, on CPU
     mine = D.padded_shard(srcs, world, rank).view(per, 1)
     out = torch.empty((world * per, 1), dtype=torch.int32)
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(max(1, args.steps)):
-        D.all_gather_rows_async(mine, out).wait()
-    dist.barrier()
-    elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-    dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    routes = float(len(srcs)) * fabric.n_hosts
+
+    def step():                             # the "step": this rank's ids assembled
+        (D.all_gather_rows_async(mine, out) if args.assemble == "all"
+         else D.gather_rows_to_root(mine, out)).wait()
+
+    def timed(reps):
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            step()
+        dist.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return float(el.item()) / reps * 1e3
+
+    ms = timed(max(1, args.steps))
+    single = timed(1)
+    by_inflight = {"1": {"steps_in_flight": 1, "ms_per_step": ms, "value": routes / (ms / 1e3),
+                         "steps": args.steps, "headline": True}}
+    base = None
+    if rank == 0:                           # rank 0 alone, all ids (meaningless rate)
+        t0 = time.perf_counter()
+        torch.from_numpy(srcs).clone()
+        b = max(1e-6, (time.perf_counter() - t0) * 1e3)
+        base = {"measured_on": "rank 0 alone (rehearsal)",
+                "inflight_1": {"steps_in_flight": 1, "ms_per_step": b,
+                               "value": routes / (b / 1e3)}}
     shards = [None] * world
     dist.all_gather_object(shards, (rank, lo, hi, os.getpid()))
-    ok = bool(np.array_equal(D.unpad(out.view(-1), len(srcs)).numpy(), srcs))
+    if args.assemble == "root":
+        ok = rank != 0 or bool(np.array_equal(D.unpad(out.view(-1), len(srcs)).numpy(), srcs))
+    else:
+        ok = bool(np.array_equal(D.unpad(out.view(-1), len(srcs)).numpy(), srcs))
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:   # as the N > 1 line: rank 0, after the steps
+        cpu = cpu_baseline(fabric, fabric.csr(), srcs, counts, fabric.n_hosts,
+                           args.cpu_budget_s)[0]
+    dist.barrier()
     if rank == 0:
+        multi = {"single_step_ms": single, "by_inflight": by_inflight,
+                 "assembly_check": check, "n1_base": base}
+        multi.update(scaling_keys(routes / (ms / 1e3), by_inflight, base, world))
         print(json.dumps({
             "metric": METRIC, "rehearsal": True, "value": None, "n_gpus": world,
-            "steps": args.steps, "ms_per_step": float(elapsed.item()) / max(1, args.steps) * 1e3,
+            "steps": args.steps, "ms_per_step": ms, "single_step_ms": single,
             "process_group": {"backend": dist.get_backend(), "world_size": dist.get_world_size()},
-            "config": {"fabric": args.fabric, "sources": len(srcs),
+            "config": {"fabric": args.fabric, "sources": len(srcs), "assemble": args.assemble,
+                       "assemble_reason": ASSEMBLE_REASON[args.assemble],
                        "parallelism": "sources sharded over %d rank(s)" % world},
+            "multi_gpu": multi, "cpu_baseline": cpu,
             "shards": [{"rank": r, "lo": a, "hi": b, "pid": p} for r, a, b, p in shards],
             "sources_assembled_exactly": ok}), flush=True)
     dist.destroy_process_group()
@@ -832,7 +941,8 @@ def pipelined_rate(local, dev, csr, t_src, per, tables, slots, packed, mode, rou
                    k=3):
     """The same step with k consecutive steps in flight on their own streams
     and library contexts (what an N > 1 rank runs), one GPU: every step
-    still computes every table of the step."""
+    still computes every table of the step.  k = 1: one step at a time,
+    back to back on one stream (the N = 1 line's own schedule)."""
     streams = [torch.cuda.Stream(dev) for _ in range(k)]
     ctxs = []
     for st in streams:
@@ -885,18 +995,20 @@ def main():
                          % (world, args.gpus))
     if args.rehearse:
         sys.exit(main_rehearse(args, world, rank) if world > 1 else 0)
+    ref_mp = None
+    if world == 1 and args.mode == "dfs" and not args.no_cpu_baseline:
+        # forks: must run before the first GPU call of this process (and so
+        # before the device count below, which may initialise HIP when
+        # torch cannot count through amdsmi)
+        ref_mp = cpu_reference_path_mp(T.by_name(args.fabric),
+                                       secs=min(5.0, args.cpu_budget_s / 4))
     # BENCH_DEVICE pins every rank to one device (rehearsing the N > 1 code
     # path on a one-GPU box); the driver never sets it
     if os.environ.get("BENCH_DEVICE"):
         local = int(os.environ["BENCH_DEVICE"])
-    elif torch.cuda.device_count() < world:      # counts devices without initialising HIP
+    elif torch.cuda.device_count() < world:
         raise SystemExit("bench.py: --gpus %d but only %d GPU(s) are visible"
                          % (world, torch.cuda.device_count()))
-    ref_mp = None
-    if world == 1 and args.mode == "dfs" and not args.no_cpu_baseline:
-        # forks: must run before the first GPU call of this process
-        ref_mp = cpu_reference_path_mp(T.by_name(args.fabric),
-                                       secs=min(5.0, args.cpu_budget_s / 4))
     torch.cuda.set_device(local)              # before the process group: its communicator
     if world > 1:                             # and every context live on this rank's GPU
         backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")   # gloo: rehearsal only
@@ -912,6 +1024,16 @@ def main():
         if len(uuids) != world and not os.environ.get("BENCH_DEVICE"):
             raise SystemExit("bench.py: %d ranks share %d device(s): %r"
                              % (world, len(uuids), devices))
+    assembly_check = None
+    if world > 1 and args.mode in ("dfs", "shortest"):
+        # both assembly forms on a small table before anything is timed: a
+        # form that raises or assembles wrong rows is reported, and the
+        # headline falls back to the other one instead of losing the line
+        assembly_check = D.check_assembly(dev)
+        other = "all" if args.assemble == "root" else "root"
+        if assembly_check.get(args.assemble) != "ok" and assembly_check.get(other) == "ok":
+            assembly_check["fallback"] = "%s -> %s" % (args.assemble, other)
+            args.assemble = other
     if args.mode == "flows":
         return main_flows(args, world, rank, local, dev)
     if args.mode == "ecmp":
@@ -952,15 +1074,15 @@ def main():
     if args.layout == "slots" and not slots:
         raise SystemExit("--layout slots: fabric has a switch with more than 63 links")
     packed = port16 or slots                  # one u32 per tree entry
-    def tables():
+    def tables(rows=per):
         if packed:
-            return (torch.empty((per, V), dtype=torch.int32, device=dev),)   # parent | port << 16
+            return (torch.empty((rows, V), dtype=torch.int32, device=dev),)   # parent | port << 16
         if args.mode == "dfs":
-            return (torch.empty((per, V), dtype=torch.int32, device=dev),    # parent
-                    torch.empty((per, V), dtype=torch.int32, device=dev))    # port
-        return (torch.empty((per, V), dtype=torch.int16, device=dev),        # dist (u16)
-                torch.empty((per, V), dtype=torch.int32, device=dev),        # nh
-                torch.empty((per, V), dtype=torch.int32, device=dev))        # nh_port
+            return (torch.empty((rows, V), dtype=torch.int32, device=dev),    # parent
+                    torch.empty((rows, V), dtype=torch.int32, device=dev))    # port
+        return (torch.empty((rows, V), dtype=torch.int16, device=dev),        # dist (u16)
+                torch.empty((rows, V), dtype=torch.int32, device=dev),        # nh
+                torch.empty((rows, V), dtype=torch.int32, device=dev))        # nh_port
 
     # N > 1: one rank's share of the k=48 sources (144 at N = 8) fills an
     # eighth of the GPU, and a source's search is a serial chain (DESIGN.md
@@ -980,6 +1102,8 @@ def main():
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     inflight = args.inflight if args.inflight > 0 else \
         (3 if world > 1 and per < 4 * cus else 1)
+    infl = [inflight]                        # steps in flight right now (the single-step
+                                             # and one-at-a-time measurements set 1)
     streams = [stream] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
     # one library context per stream in flight: a context's scratch (the split
     # kernel's spill rings and chunk cursors, the watchdog word) serves one
@@ -1000,8 +1124,8 @@ def main():
 
     def step(ev=None):
         k = counter[0] % nbuf
-        st = streams[counter[0] % inflight]   # table set k always runs on stream k % inflight
-        cx = ctxs[counter[0] % inflight]      # ... through that stream's context
+        st = streams[counter[0] % infl[0]]    # table set k runs on stream k % inflight
+        cx = ctxs[counter[0] % infl[0]]       # ... through that stream's context
         counter[0] += 1
         with torch.cuda.stream(st):
             for w in pending[k]:            # this set's previous gather is done
@@ -1028,7 +1152,7 @@ def main():
 
     def drain():
         for k in range(nbuf):
-            with torch.cuda.stream(streams[k % inflight]):
+            with torch.cuda.stream(streams[k % infl[0]]):
                 for w in pending[k]:
                     w.wait()
             pending[k] = []
@@ -1063,17 +1187,74 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     routes = float(counts.sum()) * float(H)      # every host pair of these sources
     value = routes / (ms_per_step / 1e3)
+
+    def single_step_ms():
+        """ONE step alone -- launched, assembled (N > 1) and synchronized: the
+        latency a controller waits for one fresh table set.  Median over a
+        few repetitions, max over the ranks."""
+        reps = max(3, min(20, args.steps))
+        drain()
+        torch.cuda.synchronize(dev)
+        infl[0] = 1
+        ts = []
+        for _ in range(reps):
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            step()
+            drain()
+            torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - t0)
+        infl[0] = inflight
+        ms = float(np.median(ts)) * 1e3
+        return _max_min(ms, dev)[0] if world > 1 else ms
+
+    def rate_at(k, reps):
+        """Back-to-back steps with k in flight (same assembly), ms per step
+        over the ranks' max."""
+        drain()
+        torch.cuda.synchronize(dev)
+        infl[0] = k
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            step()
+        drain()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        infl[0] = inflight
+        ms = (time.perf_counter() - t0) / reps * 1e3
+        ms = _max_min(ms, dev)[0] if world > 1 else ms
+        return {"steps_in_flight": k, "ms_per_step": ms, "value": routes / (ms / 1e3),
+                "steps": reps}
+
+    single_ms = single_step_ms()
+    by_inflight = {str(inflight): {"steps_in_flight": inflight, "ms_per_step": ms_per_step,
+                                   "value": value, "steps": args.steps, "headline": True}}
+    if inflight > 1:                          # the same ranks, one step at a time
+        by_inflight["1"] = rate_at(1, max(args.steps // 2, 10))
     pipelined = None
     set_bytes = sum(t.numel() * t.element_size() for t in bufs[0])
     if world == 1 and inflight == 1 and args.inflight == 0 and 3 * set_bytes <= (4 << 30) \
             and ms_per_step <= 10.0:      # small steps only: 3 more table sets, 30+ steps
         pipelined = pipelined_rate(local, dev, csr, t_src, per, tables, slots, packed,
                                    args.mode, routes, max(args.steps, 30))
+        by_inflight["3"] = {k: pipelined[k] for k in ("steps_in_flight", "ms_per_step",
+                                                      "value", "steps")}
     multi = None
     if world > 1:
         multi = multi_gpu_extras(args, world, rank, local, dev, csr, srcs, per, packed, slots,
                                  kern_ms, ms_per_step, routes, step, drain, bufs, gathered,
-                                 assemble)
+                                 assemble, assembly_check)
+        multi["single_step_ms"] = single_ms
+        multi["by_inflight"] = by_inflight
+        multi["assembly_check"] = assembly_check
+        multi["n1_base"] = n1_base(args, rank, local, dev, csr, srcs, tables, slots, packed,
+                                   routes, kern_ms * world)
+        multi.update(scaling_keys(value, by_inflight, multi["n1_base"], world))
     for c in ctxs[1:]:
         c.close()
     bytes_launch = algorithmic_bytes_per_source(V, E, args.mode, packed) * (hi - lo)
@@ -1134,6 +1315,8 @@ def main():
         "switch_pair_routes_per_s": float(S) * V / (ms_per_step / 1e3),
         "teps": float(hi - lo) * E / (kern_ms / 1e3),
     }
+    out["single_step_ms"] = single_ms
+    out["by_inflight"] = by_inflight
     if pipelined is not None:
         out["pipelined"] = pipelined
     if multi is not None:
@@ -1144,6 +1327,7 @@ def main():
         multi["devices"] = [{"rank": r, "local": l, "device": d} for r, l, d in devices]
         out["multi_gpu"] = multi
         out["config"]["assemble"] = args.assemble
+        out["config"]["assemble_reason"] = ASSEMBLE_REASON[args.assemble]
     if rank == 0 and world == 1 and args.mode == "dfs" and \
             float(S) * V * (4 if packed else 8) <= 4e9:
         # the drop-in's host-buffer boundary: sources in, tables out over PCIe
@@ -1176,7 +1360,11 @@ def main():
     if rank == 0 and world == 1 and args.mode == "dfs" and not args.max_sources and \
             not args.no_flows and not args.all_vertices and args.fabric.startswith("fat_tree"):
         out["dropin"] = dropin_block(fabric)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.mode == "dfs":
+    if world > 1 and not args.no_cpu_baseline and args.mode == "dfs":
+        dist.barrier()         # the GPU work of every rank is done: rank 0 alone on the host
+    if rank == 0 and not args.no_cpu_baseline and args.mode == "dfs":
+        # N > 1 too (north_star: the host-CPU baseline "in the same run"):
+        # pthreads and plain loops, no fork, after every rank's timed work
         base, ref, ref_pred = cpu_baseline(fabric, csr, srcs, counts, H, args.cpu_budget_s)
         if "dropin" in out:   # the reference's own cost per query, beside the drop-in's
             out["dropin"]["cpu_reference_ms_per_route"] = 1e3 / ref["value"]
@@ -1186,6 +1374,8 @@ def main():
         if ref_mp is not None:
             out["cpu_reference_path_all_cores"] = ref_mp
         out["gpu_over_cpu"] = value / base["value"]
+    if world > 1 and not args.no_cpu_baseline and args.mode == "dfs":
+        dist.barrier()
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

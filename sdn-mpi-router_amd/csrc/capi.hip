@@ -43,11 +43,13 @@ int sdnr_check_watchdog(sdnr_ctx *ctx)
     SDNR_HIP(hipMemcpy(&h, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (h) {
         SDNR_HIP(hipMemset(ctx->d_err, 0, sizeof(int)));
-        if (h == kErrTreeClimb)
+        // bit tests: a word may hold several codes (e.g. a bad last port and
+        // a hand-off wait of the same expansion); the specific cause wins
+        if (h & kErrTreeClimb)
             return sdnr_fail(SDNR_ERR_INVAL, "sdnr_dfs_rows_affected: a tree row is not a tree "
                              "(a parent chain longer than V, or a reached vertex without a "
                              "reached parent)");
-        if (h == kErrLastPort)
+        if (h & kErrLastPort)
             return sdnr_fail(SDNR_ERR_INVAL, "sdnr_route_expand_packed: a last port outside "
                              "[0, 0xFFFF] (u32 entries hold 16-bit ports): entries invalid");
         return sdnr_fail(SDNR_ERR_HIP, "kernel watchdog tripped (code %d): results invalid", h);

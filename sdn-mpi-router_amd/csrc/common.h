@@ -131,8 +131,9 @@ inline void sdnr_allow_lds(const void *fn, size_t bytes)
 }
 
 // watchdog-word codes a kernel ORs into ctx->d_err (dfs.hip uses 1..16 for
-// bounded waits that ran out); sdnr_synchronize turns a nonzero word into an
-// error
+// bounded waits that ran out, and 32 for the split kernel's CU-numbering spin,
+// split_cu_number); sdnr_synchronize turns a nonzero word into an error, the
+// specific INVAL causes below tested bit by bit (a word may hold several)
 constexpr int kErrLastPort = 256;   // sdnr_route_expand_packed: a last port outside [0, 0xFFFF]
 constexpr int kErrTreeClimb = 512;  // sdnr_dfs_rows_affected: a tree climb outran V steps
 constexpr int kErrScan = 1024;      // sdnr_route_offsets: a look-back wait ran out

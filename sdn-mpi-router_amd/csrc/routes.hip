@@ -1054,6 +1054,10 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
         const bool reuse = same_tables && ctx->anc_valid && ctx->anc_parent == d_parent &&
                            ctx->anc_port == d_port && ctx->anc_n == n;
         if (!reuse) {
+            // invalid until the rebuild below is launched: a failed reserve
+            // (which frees the old buffer) or launch must not leave a later
+            // SDNR_SAME_TABLES call matching the old tables
+            ctx->anc_valid = false;
             int rc = sdnr_reserve(&ctx->anc, &ctx->anc_bytes, 14 * n + 64);
             if (rc) return rc;
         }
@@ -1070,6 +1074,7 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
                 hipLaunchKernelGGL(tree_compose16_kernel, dim3(cg), dim3(256), 0, ctx->stream,
                                    ctx->V, n, prev, prev, a16 + (size_t)j * n);
             }
+            SDNR_HIP(hipGetLastError());
             ctx->anc_parent = d_parent;
             ctx->anc_port = d_port;
             ctx->anc_n = n;

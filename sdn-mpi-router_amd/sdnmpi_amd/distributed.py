@@ -15,7 +15,7 @@ import torch
 import torch.distributed as dist
 
 __all__ = ["shard_bounds", "padded_shard", "all_gather_rows", "all_gather_rows_async", "unpad",
-           "sharded_route_tables", "gather_rows_to_root"]
+           "sharded_route_tables", "gather_rows_to_root", "check_assembly"]
 
 
 def shard_bounds(n, world, rank):
@@ -128,6 +128,43 @@ def gather_rows_to_root(local, out, group=None, root=0):
     if rank == root:
         out.copy_(torch.cat(parts).to(out.device))
     return _Done()
+
+
+def check_assembly(device=None, group=None, forms=("root", "all")):
+    """Preflight of the two assembly forms on a small table (a few rows of
+    rank-specific values): {"root": "ok" | error, "all": "ok" | error}.  A
+    form that raises, or that assembles the wrong rows, is reported instead
+    of failing the caller; bench.py runs this before its timed loop and
+    falls back to the other form when the headline one is broken."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    rows, cols = 3, 5
+    local = (torch.arange(rows * cols, dtype=torch.int32).view(rows, cols) + 1000 * rank)
+    want = torch.cat([torch.arange(rows * cols, dtype=torch.int32).view(rows, cols) + 1000 * r
+                      for r in range(world)])
+    if device is not None:
+        local = local.to(device)
+    res = {}
+    for form in forms:
+        try:
+            out = torch.full((world * rows, cols), -7, dtype=torch.int32, device=local.device)
+            (all_gather_rows_async(local, out, group) if form == "all"
+             else gather_rows_to_root(local, out, group)).wait()
+            if local.is_cuda:
+                torch.cuda.synchronize(local.device)
+            if form == "all" or rank == 0:
+                ok = bool(torch.equal(out.cpu(), want))
+            else:
+                ok = True
+            # every rank learns whether the root (or any rank) saw a wrong table
+            flag = torch.tensor([0 if ok else 1], dtype=torch.int32,
+                                device=local.device if dist.get_backend(group) == "nccl"
+                                else "cpu")
+            dist.all_reduce(flag, group=group)
+            res[form] = "ok" if int(flag.item()) == 0 else "wrong rows assembled"
+        except Exception as e:   # noqa: BLE001 -- reported to the caller
+            res[form] = "error: " + repr(e)[:200]
+    return res
 
 
 def unpad(table, n):

@@ -30,9 +30,10 @@ def _run(args, env, timeout=300):
                           env=env, capture_output=True, text=True, timeout=timeout)
 
 
-@pytest.mark.parametrize("n", [2, 3])
-def test_bench_gpus_n_launches_n_ranks(n):
-    r = _run(["--gpus", str(n), "--rehearse", "--steps", "2"], _env())
+@pytest.mark.parametrize("n,form", [(2, "root"), (3, "root"), (2, "all")])
+def test_bench_gpus_n_launches_n_ranks(n, form):
+    r = _run(["--gpus", str(n), "--rehearse", "--steps", "2", "--assemble", form,
+              "--cpu-budget-s", "2"], _env())
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout           # rank 0 alone prints the line
@@ -45,6 +46,19 @@ def test_bench_gpus_n_launches_n_ranks(n):
     assert line["shards"][0]["lo"] == 0 and line["shards"][-1]["hi"] == 1152
     assert all(a["hi"] == b["lo"] for a, b in zip(line["shards"], line["shards"][1:]))
     assert line["sources_assembled_exactly"] is True
+    # the N > 1 line's honesty keys: one step's latency, the
+    # rate by steps in flight, both assembly forms preflighted, the scaling
+    # efficiency against the same run's N = 1 base, why this assembly, and
+    # the host-CPU baseline measured on rank 0 in the same run
+    m = line["multi_gpu"]
+    assert line["single_step_ms"] > 0 and m["single_step_ms"] == line["single_step_ms"]
+    assert m["by_inflight"]["1"]["headline"] is True
+    assert m["assembly_check"] == {"root": "ok", "all": "ok"}
+    assert m["n1_base"]["inflight_1"]["value"] > 0
+    assert m["scaling_efficiency"] > 0 and m["scaling_efficiency_base"] == "n1_base.inflight_1"
+    assert line["config"]["assemble"] == form and line["config"]["assemble_reason"]
+    cpu = line["cpu_baseline"]
+    assert cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] == "port"
 
 
 def test_bench_refuses_world_size_mismatch():

@@ -56,6 +56,34 @@ def hbm_bytes(c):
     return (FETCH_FACTOR * c.get("FETCH_SIZE", 0.0) + WRITE_FACTOR * c.get("WRITE_SIZE", 0.0)) * 1024.0
 
 
+def coalescing(c):
+    """Read-coalescing figures of one kernel (north_star: "rocprof counters
+    must show coalesced CSR reads"), from the per-dispatch counter means:
+    * tag_lookups_per_vmem: L1 (TCP) cache-line tag lookups per wavefront
+      memory instruction, TCP_TOTAL_CACHE_ACCESSES / (SQ_INSTS_VMEM_RD +
+      SQ_INSTS_VMEM_WR).  The TCP looks a 64-lane instruction up one
+      quarter-wave at a time, so 4 is the floor: every quarter-wave in ONE
+      128-B line (a u16 row of 64 lanes, or 4-B words of 32 consecutive
+      lanes); a 16-B-per-lane copy is 8; a gather with every lane in its own
+      line is 64 (measured: rocclr's copy kernel 9.3, dfs_async 4.3);
+    * l2_req_per_vmem_rd: TCP->L2 read requests per wavefront load
+      (TCP_TCC_READ_REQ / SQ_INSTS_VMEM_RD): what leaves the CU's L1;
+    * l1_read_hit: 1 - TCP_TCC_READ_REQ / TCP_TOTAL_READ (TCP_TOTAL_READ
+      counts read accesses, hits included)."""
+    out = collections.OrderedDict()
+    req = c.get("TCP_TCC_READ_REQ_sum")
+    vm = c.get("SQ_INSTS_VMEM_RD")
+    tags = c.get("TCP_TOTAL_CACHE_ACCESSES_sum")
+    if tags is not None and vm:
+        out["tag_lookups_per_vmem"] = tags / (vm + c.get("SQ_INSTS_VMEM_WR", 0.0))
+    if req is not None and vm:
+        out["l2_req_per_vmem_rd"] = req / vm
+    rd = c.get("TCP_TOTAL_READ_sum")
+    if rd and req is not None:
+        out["l1_read_hit"] = 1.0 - req / rd
+    return out
+
+
 def main(src, out):
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     stats = os.path.join(src, "trace", "run_kernel_stats.csv")
@@ -94,6 +122,9 @@ def main(src, out):
             lines.append("- HBM traffic per dispatch (FETCH_SIZE x %.3g + WRITE_SIZE x %.3g, "
                          "factors measured by tools/calib_traffic.hip): %.1f MB"
                          % (FETCH_FACTOR, WRITE_FACTOR, hbm_bytes(c) / 1e6))
+        co = coalescing(c)
+        if co:
+            lines.append("- coalescing: " + ", ".join("%s %.3g" % kv for kv in co.items()))
         if "SQ_WAVE_CYCLES" in c:
             wc = c["SQ_WAVE_CYCLES"]
             lines.append("- wave-cycle split: wait %.0f%%, issue-stall %.0f%%, active %.0f%%" % (
