@@ -10,6 +10,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <array>
+#include <map>
 #include <string>
 #include <thread>
 #include <vector>
@@ -130,6 +132,15 @@ static void free_graph(sdnr_ctx *c)
     c->radjw = nullptr;
     if (c->radjc) (void)hipFree(c->radjc);
     c->radjc = nullptr;
+    if (c->dict_bp) (void)hipFree(c->dict_bp);
+    if (c->dict_bt) (void)hipFree(c->dict_bt);
+    if (c->dict_off) (void)hipFree(c->dict_off);
+    c->dict_bp = nullptr;
+    c->dict_bt = nullptr;
+    c->dict_off = nullptr;
+    c->dict_P = 0;
+    c->dict_NB = 0;
+    c->dict_bpw = 0;
     if (c->ell16) (void)hipFree(c->ell16);
     if (c->ell_hi) (void)hipFree(c->ell_hi);
     c->ell16 = nullptr;
@@ -371,6 +382,76 @@ int sdnr_device_list(const sdnr_ctx *ctx, int *devices, int cap, int *n)
 static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_ptr,
                             const int32_t *col, const int32_t *port);
 
+// Dictionary rows for the split DFS (dfs.hip, kRowDict): every sorted row as
+// u + D[p(u)], D a list of distinct signed neighbour-offset tuples.  A
+// regular fabric has few: a 32^3 torus 27 (3 boundary cases per dimension;
+// the wrap-around links keep their place in the sorted row because the
+// tuple is of the sorted ids' offsets).  The pattern ids are a second
+// dictionary level: blocks of 32 consecutive switches as tuples of 32
+// pattern bytes (a 32^3 torus: 9 distinct x-lines), so a switch's pattern is
+// bt[bp[u >> 5]][u & 31] and the whole form -- V / 32 block bytes, the block
+// tuples and D -- takes ~1.4 KB of LDS for the 32^3 torus (a flat byte per
+// switch, 32 KB, halved the workgroups per CU and measured slower: 99.5 vs
+// 86.6 ms).  Then a DFS window reads no row from L2.  Built when V <= 65535,
+// rows have <= 8 slots and both levels have <= kDictMaxP entries (else the
+// split kernel keeps its ELL rows -- e.g. the Jellyfish); SDNROUTE_DFS_DICT=0
+// skips it (A/B).
+static int upload_dict(sdnr_ctx *ctx, int32_t V, int32_t W, const int32_t *row_ptr,
+                       const int32_t *col)
+{
+    if (V > 65535 || W > 8) return SDNR_OK;
+    if (const char *f = getenv("SDNROUTE_DFS_DICT"))
+        if (!strcmp(f, "0")) return SDNR_OK;
+    std::map<std::array<int32_t, 8>, int> ids;
+    std::vector<std::array<int32_t, 8>> tuples;
+    std::vector<uint8_t> pat(((size_t)V + 31) & ~(size_t)31, 0);
+    for (int32_t u = 0; u < V; ++u) {
+        std::array<int32_t, 8> t;
+        t.fill(kDictPad);
+        for (int32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) t[e - row_ptr[u]] = col[e] - u;
+        auto it = ids.find(t);
+        if (it == ids.end()) {
+            if ((int)tuples.size() >= kDictMaxP) return SDNR_OK;     // irregular: ELL rows
+            it = ids.emplace(t, (int)tuples.size()).first;
+            tuples.push_back(t);
+        }
+        pat[(size_t)u] = (uint8_t)it->second;
+    }
+    const size_t nblk = pat.size() / 32;
+    std::map<std::array<uint8_t, 32>, int> bids;
+    std::vector<std::array<uint8_t, 32>> blocks;
+    const int32_t bpw = (int32_t)((nblk + 3) / 4);
+    std::vector<uint32_t> bp((size_t)bpw, 0u);
+    for (size_t b = 0; b < nblk; ++b) {
+        std::array<uint8_t, 32> t;
+        memcpy(t.data(), &pat[b * 32], 32);
+        auto it = bids.find(t);
+        if (it == bids.end()) {
+            if ((int)blocks.size() >= kDictMaxP) return SDNR_OK;
+            it = bids.emplace(t, (int)blocks.size()).first;
+            blocks.push_back(t);
+        }
+        bp[b >> 2] |= (uint32_t)it->second << (8 * (b & 3));
+    }
+    std::vector<uint32_t> bt(blocks.size() * 8);
+    for (size_t b = 0; b < blocks.size(); ++b) memcpy(&bt[b * 8], blocks[b].data(), 32);
+    std::vector<int32_t> off(tuples.size() * 8);
+    for (size_t p = 0; p < tuples.size(); ++p)
+        for (int k = 0; k < 8; ++k) off[p * 8 + k] = tuples[p][k];
+    int rc;
+    if ((rc = upload(reinterpret_cast<int32_t **>(&ctx->dict_bp), bp.data(), bp.size() * 4, 0,
+                     ctx->stream)) ||
+        (rc = upload(reinterpret_cast<int32_t **>(&ctx->dict_bt), bt.data(), bt.size() * 4, 0,
+                     ctx->stream)) ||
+        (rc = upload(&ctx->dict_off, off.data(), off.size() * 4, 0, ctx->stream)))
+        return rc;
+    SDNR_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->dict_P = (int32_t)tuples.size();
+    ctx->dict_NB = (int32_t)blocks.size();
+    ctx->dict_bpw = bpw;
+    return SDNR_OK;
+}
+
 int sdnr_graph_upload(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *row_ptr,
                       const int32_t *col, const int32_t *port)
 {
@@ -469,6 +550,10 @@ static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *
             }
         }
         SDNR_HIP(hipStreamSynchronize(ctx->stream));   // before ec/ep go away
+        if ((rc = upload_dict(ctx, V, W, row_ptr, col))) {
+            free_graph(ctx);
+            return rc;
+        }
     }
     // u16 rows of stride 64 (one 128-byte line) for the cooperative DFS
     // kernels: padding and the extra row V hold the sentinel vertex V; the

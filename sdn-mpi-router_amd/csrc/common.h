@@ -55,6 +55,15 @@ struct sdnr_ctx {
     int32_t *ell_col = nullptr, *ell_port = nullptr;
     uint16_t *ell16 = nullptr;          // ELL ids as u16 (low 16 bits when V > 65535), 0xFFFF pad
     uint32_t *ell_hi = nullptr;         // per row: the 17th id bit of each slot (65535 <= V < 131071)
+    // dictionary rows for the split DFS (V <= 65535, rows of <= 8 slots):
+    // row u = u + dict_off[p(u) * 8 + slot], p(u) = byte (u & 31) of block
+    // tuple dict_bt[b(u)] (32 pattern bytes = 8 u32 words), b(u) = byte
+    // u >> 5 of dict_bp (4 block ids per u32 word, dict_bpw words); dict_off
+    // dict_P x 8 int32 offsets (padding slots: kDictPad)
+    uint32_t *dict_bp = nullptr;
+    uint32_t *dict_bt = nullptr;
+    int32_t *dict_off = nullptr;
+    int32_t dict_P = 0, dict_NB = 0, dict_bpw = 0;
     uint16_t *adj16 = nullptr;          // (V+1) rows x 64 u16, sentinel V (V < 65535)
     uint16_t *radj16 = nullptr;         // in-neighbour rows, same layout (== adj16 if symmetric)
     uint32_t *deg32 = nullptr;          // out-degrees of 0..V (sentinel V: 0)
@@ -134,6 +143,8 @@ inline void sdnr_allow_lds(const void *fn, size_t bytes)
 // bounded waits that ran out, and 32 for the split kernel's CU-numbering spin,
 // split_cu_number); sdnr_synchronize turns a nonzero word into an error, the
 // specific INVAL causes below tested bit by bit (a word may hold several)
+constexpr int kDictPad = 0x40000000;   // dictionary-row padding offset (u + pad >= V)
+constexpr int kDictMaxP = 255;         // pattern ids are bytes
 constexpr int kErrLastPort = 256;   // sdnr_route_expand_packed: a last port outside [0, 0xFFFF]
 constexpr int kErrTreeClimb = 512;  // sdnr_dfs_rows_affected: a tree climb outran V steps
 constexpr int kErrScan = 1024;      // sdnr_route_offsets: a look-back wait ran out

@@ -27,6 +27,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -1052,6 +1054,9 @@ __global__ __launch_bounds__(64) void dfs_global_packed_kernel(
 // batched pop of dfs_global_packed_kernel (first live entry from the top).
 // ---------------------------------------------------------------------------
 constexpr int kRow32 = 0, kRow16 = 1, kRow17 = 2;
+// dictionary rows (split kernel, rows of <= 8 slots): row u = u + D[p(u)],
+// the pattern ids and D staged in LDS (capi.hip upload_dict)
+constexpr int kRowDict = 3;
 constexpr int kSplitQ = 64;                    // queued records per search wave
 // SDNROUTE_DFS_FLAGS (tuning): search waves at raised issue priority,
 // non-temporal table stores, or (diagnostic) no table stores at all / port
@@ -1186,12 +1191,25 @@ template <> struct SplitRing<false> {
     static __device__ __forceinline__ T put(uint32_t v, uint32_t) { return v; }
 };
 
-__host__ __device__ constexpr bool split_wide_ring(int lpr, bool hops) { return hops || lpr == 8; }
+// dictionary rows without hop counts: one u32 per entry, vertex | pattern
+// << 16 (V <= 65535) -- the narrow ring keeps the 32^3 torus at 4 workgroups
+// per CU with the dictionary's LDS added
+struct SplitRingDict {
+    using T = uint32_t;
+    static __device__ __forceinline__ uint2 get(T e) { return make_uint2(e & 0xFFFFu, e >> 16); }
+    static __device__ __forceinline__ T put(uint32_t v, uint32_t y) { return v | (y << 16); }
+};
 
-__host__ __device__ inline size_t split_lds_words(int V, int ring, int ns, bool hops, int lpr)
+__host__ __device__ constexpr bool split_wide_ring(int lpr, bool hops, bool dict = false)
+{
+    return hops || (lpr == 8 && !dict);
+}
+
+__host__ __device__ inline size_t split_lds_words(int V, int ring, int ns, bool hops, int lpr,
+                                                  bool dict = false)
 {
     const size_t VWp = (size_t)((((V + 31) >> 5) + 31) & ~31);
-    return (size_t)ns * (VWp + (split_wide_ring(lpr, hops) ? 2 : 1) * (size_t)ring) +
+    return (size_t)ns * (VWp + (split_wide_ring(lpr, hops, dict) ? 2 : 1) * (size_t)ring) +
            (size_t)ns * kSplitQ * (hops ? 3 : 2) +
            ((3 * (size_t)ns + 3) & ~(size_t)3);
 }
@@ -1202,7 +1220,13 @@ constexpr int kTreeInt32 = 0, kTreePort16 = 1, kTreeSlot = 2;
 
 // The writer wave of the split kernels: drains the NS search waves' record
 // queues (vertex | slot << 26, parent[, depth]) into the table rows, loading
-// the port of each tree edge off the search chain.
+// the port of each tree edge off the search chain.  One round takes the
+// records of ALL queues at once, packed into the 64 lanes (queue k's pending
+// records after queue k-1's), so a round is one LDS read -> port load ->
+// store chain however many queues have records (round 5 drained the queues
+// one after the other: NS dependent port-load round trips per round, and
+// with dictionary rows -- a search twice as fast -- the search waves then
+// waited 929 cycles per push for queue room; stamps).
 template <int NS, bool HOPS, int PK>
 __device__ __forceinline__ void split_writer(int V, int W, const int32_t *__restrict__ ell_port,
                                              const uint2 *qrec, const uint32_t *qdep, int *ctl,
@@ -1211,93 +1235,110 @@ __device__ __forceinline__ void split_writer(int V, int W, const int32_t *__rest
                                              int32_t *__restrict__ out_hops, int *__restrict__ err,
                                              int flags)
 {
+    static_assert(NS <= 32, "one lane per queue");
     constexpr unsigned kIdle = 1u << 26;
     constexpr bool PACKED = PK != kTreeInt32;
-    int consd[NS];
-#pragma unroll
-    for (int k = 0; k < NS; ++k) consd[k] = 0;
+    int consd = 0;                     // lane k < NS: records of queue k consumed
     unsigned idle = 0;
     for (;;) {
-        bool any = false, all_done = true;
+        // records first, then the row: a source's row is announced before
+        // its first record, and changes only after the writer consumed all
+        // of the previous source's records
+        int P = 0, row = -1;
+        if (lane < NS) {
+            P = __hip_atomic_load(&ctl[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            row = __hip_atomic_load(&ctl[2 * NS + lane], __ATOMIC_ACQUIRE,
+                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        const int avail = lane < NS ? P - consd : 0;
+        // exclusive prefix of the queues' pending records over lanes 0..NS-1
+        int incl = avail;
 #pragma unroll
-        for (int k = 0; k < NS; ++k) {
-            // records first, then the row: a source's row is announced
-            // before its first record, and changes only after the
-            // writer consumed all of the previous source's records
-            const int P = __hip_atomic_load(&ctl[k], __ATOMIC_ACQUIRE,
-                                            __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int row = __hip_atomic_load(&ctl[2 * NS + k], __ATOMIC_ACQUIRE,
-                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int C = consd[k];
-            if (P > C) {
-                any = true;
-                all_done = false;
-                const int n = P - C < SDNR_WAVE ? P - C : SDNR_WAVE;
-                if (lane < n) {
-                    const int at = k * kSplitQ + ((C + lane) & (kSplitQ - 1));
-                    const uint2 r = qrec[at];
-                    const int v = (int)(r.x & 0x3FFFFFFu), slot = (int)(r.x >> 26);
-                    const int par = (int)r.y;
-                    const size_t e = (size_t)row * V + v;
-                    if (PK == kTreeSlot) {     // no port lookup: the slot names it
-                        const int32_t tv = (int32_t)((uint32_t)par | ((uint32_t)slot << 26));
-                        if (flags & kFlagNT) __builtin_nontemporal_store(tv, &out_parent[e]);
-                        else if (!(flags & kFlagNoStore)) out_parent[e] = tv;
-                        if (HOPS && !(flags & kFlagNoStore)) put_hop(out_hops, e, (int)qdep[at], flags);
-                    } else {
-                        const int pt = (flags & kFlagNoPort) ? slot
-                                                             : ell_port[(size_t)par * W + slot];
-                        if (flags & kFlagNoStore) {
-                            // diagnostic: records consumed, no table stores
-                        } else if (flags & kFlagNT) {
-                            if (PACKED) {
-                                __builtin_nontemporal_store(
-                                    (int32_t)(((uint32_t)par & 0xFFFFu) | ((uint32_t)pt << 16)),
-                                    &out_parent[e]);
-                            } else {
-                                __builtin_nontemporal_store(par, &out_parent[e]);
-                                __builtin_nontemporal_store(pt, &out_port[e]);
-                            }
-                            if (HOPS) {
-                                if (flags & kFlagHops16)
-                                    __builtin_nontemporal_store(
-                                        (uint16_t)qdep[at], reinterpret_cast<uint16_t *>(out_hops) + e);
-                                else
-                                    __builtin_nontemporal_store((int)qdep[at], &out_hops[e]);
-                            }
+        for (int d = 1; d < NS; d <<= 1) {
+            const int t = __shfl_up(incl, d);
+            if (lane >= d) incl += t;
+        }
+        const int excl = incl - avail;
+        const int total = read_lane(incl, NS - 1);
+        if (total > 0) {
+            // lane l serves record l of the packed list: queue k with
+            // excl_k <= l < excl_k + avail_k (a uniform scan over the queues)
+            int k = -1, idx = 0, crow = 0, cbase = 0;
+#pragma unroll
+            for (int q = 0; q < NS; ++q) {
+                const int e = read_lane(excl, q), a = read_lane(avail, q);
+                if (lane >= e && lane < e + a) {
+                    k = q;
+                    idx = lane - e;
+                    crow = read_lane(row, q);
+                    cbase = read_lane(consd, q);
+                }
+            }
+            if (k >= 0) {
+                const int at = k * kSplitQ + ((cbase + idx) & (kSplitQ - 1));
+                const uint2 r = qrec[at];
+                const int v = (int)(r.x & 0x3FFFFFFu), slot = (int)(r.x >> 26);
+                const int par = (int)r.y;
+                const size_t e = (size_t)crow * V + v;
+                if (PK == kTreeSlot) {         // no port lookup: the slot names it
+                    const int32_t tv = (int32_t)((uint32_t)par | ((uint32_t)slot << 26));
+                    if (flags & kFlagNT) __builtin_nontemporal_store(tv, &out_parent[e]);
+                    else if (!(flags & kFlagNoStore)) out_parent[e] = tv;
+                    if (HOPS && !(flags & kFlagNoStore)) put_hop(out_hops, e, (int)qdep[at], flags);
+                } else {
+                    const int pt = (flags & kFlagNoPort) ? slot : ell_port[(size_t)par * W + slot];
+                    if (flags & kFlagNoStore) {
+                        // diagnostic: records consumed, no table stores
+                    } else if (flags & kFlagNT) {
+                        if (PACKED) {
+                            __builtin_nontemporal_store(
+                                (int32_t)(((uint32_t)par & 0xFFFFu) | ((uint32_t)pt << 16)),
+                                &out_parent[e]);
                         } else {
-                            if (PACKED) {
-                                out_parent[e] = (int32_t)(((uint32_t)par & 0xFFFFu) |
-                                                          ((uint32_t)pt << 16));
-                            } else {
-                                out_parent[e] = par;
-                                out_port[e] = pt;
-                            }
-                            if (HOPS) put_hop(out_hops, e, (int)qdep[at], flags);
+                            __builtin_nontemporal_store(par, &out_parent[e]);
+                            __builtin_nontemporal_store(pt, &out_port[e]);
                         }
+                        if (HOPS) {
+                            if (flags & kFlagHops16)
+                                __builtin_nontemporal_store(
+                                    (uint16_t)qdep[at], reinterpret_cast<uint16_t *>(out_hops) + e);
+                            else
+                                __builtin_nontemporal_store((int)qdep[at], &out_hops[e]);
+                        }
+                    } else {
+                        if (PACKED) {
+                            out_parent[e] = (int32_t)(((uint32_t)par & 0xFFFFu) |
+                                                      ((uint32_t)pt << 16));
+                        } else {
+                            out_parent[e] = par;
+                            out_port[e] = pt;
+                        }
+                        if (HOPS) put_hop(out_hops, e, (int)qdep[at], flags);
                     }
                 }
-                consd[k] = C + n;
-                // the record reads above are done (LDS ops in order)
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-                if (lane == 0) __hip_atomic_store(&ctl[NS + k], C + n, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else if (row != -1 ||
-                       __hip_atomic_load(&ctl[k], __ATOMIC_ACQUIRE,
-                                         __HIP_MEMORY_SCOPE_WORKGROUP) != C) {
-                all_done = false;              // running, or published meanwhile
             }
-        }
-        if (all_done) break;
-        if (any) {
+            // queue k's share of this round (the list is cut at 64 lanes)
+            const int took = lane < NS ? max(0, min(avail, SDNR_WAVE - excl)) : 0;
+            consd += took;
+            // the record reads above are done (LDS ops in order)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            if (took > 0) __hip_atomic_store(&ctl[NS + lane], consd, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
             idle = 0;
-        } else {
-            if (++idle > kIdle) {
-                if (lane == 0) atomicOr(err, 16);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
+            continue;
         }
+        // nothing pending: done when every queue's wave has finished (row
+        // -1) and published nothing meanwhile
+        bool done = true;
+        if (lane < NS)
+            done = row == -1 && __hip_atomic_load(&ctl[lane], __ATOMIC_ACQUIRE,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP) == consd;
+        if (__ballot(!done) == 0ull) break;
+        if (++idle > kIdle) {
+            if (lane == 0) atomicOr(err, 16);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
     }
 }
 
@@ -1307,8 +1348,18 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
     const int32_t *__restrict__ ell_port, const int32_t *__restrict__ src, int nsrc,
     int32_t *__restrict__ out_parent, int32_t *__restrict__ out_port,
     int32_t *__restrict__ out_hops, uint2 *__restrict__ spill_all, int *__restrict__ err,
-    int flags, int *__restrict__ wq, int nch)
+    int flags, int *__restrict__ wq, int nch, const uint32_t *__restrict__ dict_bp,
+    const uint32_t *__restrict__ dict_bt, const int32_t *__restrict__ dict_off, int dict_bpw,
+    int dict_NB, int dict_P)
 {
+    // kRowDict: a stack entry carries its vertex's pattern id (ring .y =
+    // pattern | depth << 8), a window's row is u + D[pattern][slot] from LDS
+    // and the new children's pattern ids (two dictionary levels, capi.hip
+    // upload_dict) are read beside their visited words, so the chain touches
+    // no global memory (the torus's window was one dependent
+    // L2 row read at the loaded L2 latency)
+    constexpr bool DICT = FMT == kRowDict;
+    static_assert(!DICT || LPR == 8, "dictionary rows: 8 lanes per row");
     constexpr int R = 64 / LPR;
     constexpr int K = R * J;
     constexpr unsigned kSpin = 1u << 22;
@@ -1317,8 +1368,11 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int VW = (V + 31) >> 5;
     const int VWp = (VW + 31) & ~31;          // whole 32-word blocks (swizzled)
-    constexpr bool WR = split_wide_ring(LPR, HOPS);
-    using RE = SplitRing<WR>;
+    constexpr bool WR = split_wide_ring(LPR, HOPS, DICT);
+    // entries carry (vertex, y): y = depth, or with dictionary rows the
+    // pattern id (| depth << 8 with hop counts: the wide ring)
+    constexpr bool YR = WR || DICT;
+    using RE = typename std::conditional<DICT && !WR, SplitRingDict, SplitRing<WR>>::type;
     using RT = typename RE::T;
     const int per = VWp + (WR ? 2 : 1) * RING;   // words per search wave: vis | stack ring
     uint2 *qrec = reinterpret_cast<uint2 *>(lds + NS * per);
@@ -1327,10 +1381,27 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
     // writer consumed, ctl[2NS + k] table row of wave k's source (-2 none
     // yet, -1 no more)
     int *ctl = reinterpret_cast<int *>(qdep + (HOPS ? NS * kSplitQ : 0));
+    // dictionary: block ids (4 per word), block tuples (8 words each), then
+    // D (8 offsets per pattern id)
+    uint32_t *lbp = reinterpret_cast<uint32_t *>(ctl) + ((3 * NS + 3) & ~3);
+    uint32_t *lbt = lbp + (DICT ? dict_bpw : 0);
+    const int32_t *loff = reinterpret_cast<const int32_t *>(lbt + (DICT ? 8 * dict_NB : 0));
     const int lane = lane_id();
     const int w = uniform((int)(threadIdx.x >> 6));
     if (threadIdx.x < 3 * NS) ctl[threadIdx.x] = (int)threadIdx.x >= 2 * NS ? -2 : 0;
+    if (DICT) {
+        for (int i = threadIdx.x; i < dict_bpw; i += blockDim.x) lbp[i] = dict_bp[i];
+        for (int i = threadIdx.x; i < 8 * dict_NB; i += blockDim.x) lbt[i] = dict_bt[i];
+        int32_t *lo = reinterpret_cast<int32_t *>(lbt + 8 * dict_NB);
+        for (int i = threadIdx.x; i < dict_P * 8; i += blockDim.x) lo[i] = dict_off[i];
+    }
     __syncthreads();
+    // pattern id of v in [0, V): block id, then the block tuple's byte
+    auto blk_of = [&](int v) -> uint32_t { return (lbp[v >> 7] >> (8 * ((v >> 5) & 3))) & 0xFFu; };
+    auto pat_in = [&](uint32_t b, int v) -> uint32_t {
+        return (lbt[b * 8 + ((v & 31) >> 2)] >> (8 * (v & 3))) & 0xFFu;
+    };
+    auto pat_of = [&](int v) -> uint32_t { return pat_in(blk_of(v), v); };
 
     if (w < NS) {
         // ------------------------------------------------------ a search wave
@@ -1377,7 +1448,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                         : PK == kTreeSlot  ? (int32_t)((uint32_t)s | (63u << 26)) : s;
                 if (!PACKED) trow[s] = -1;
                 if (HOPS) put_hop(out_hops, hb + s, 0, flags);
-                ring[0] = RE::put((uint32_t)s, 0u);
+                ring[0] = RE::put((uint32_t)s, DICT ? pat_of(s) : 0u);
                 __hip_atomic_store(&ctl[2 * NS + w], si, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
             }
@@ -1387,7 +1458,12 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                 if (lsp == 0) {
                     if (gsp == 0) break;
                     const int n = gsp < RING / 2 ? gsp : RING / 2;
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // own spill stores
+                    // own spill stores: this wave wrote them through this
+                    // CU's L1, so a workgroup-scope acquire (wait for them;
+                    // no L1 invalidate) suffices -- the agent-scope one cost
+                    // ~9.7 k cycles per refill under the writers' store
+                    // traffic (stamps)
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                     bot = (bot - n) & (RING - 1);
 #ifdef SDNR_STAMPS
                     SDNR_STAMP(z_a);
@@ -1417,27 +1493,42 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                 if (J == 1) {
                     ue[0] = RE::get(ring[(bot + lsp - 1 - sub) & (RING - 1)]);
                     ue[0].x = sub < kk ? ue[0].x : 0u;
+                    if (DICT) ue[0].y = sub < kk ? ue[0].y : 0u;
                 } else {
                     uint2 me = RE::get(ring[(bot + lsp - 1 - lane) & (RING - 1)]);
                     me.x = lane < kk ? me.x : 0u;
+                    if (DICT) me.y = lane < kk ? me.y : 0u;
 #pragma unroll
                     for (int j = 0; j < J; ++j) {
                         ue[j].x = (uint32_t)__shfl((int)me.x, j * R + sub);
-                        ue[j].y = WR ? (uint32_t)__shfl((int)me.y, j * R + sub) : 0u;
+                        ue[j].y = YR ? (uint32_t)__shfl((int)me.y, j * R + sub) : 0u;
                     }
                 }
 #pragma unroll
-                for (int j = 0; j < J; ++j) x[j] = split_row<FMT>(rows, rhi, V, W, (int)ue[j].x, pos);
+                for (int j = 0; j < J; ++j) {
+                    if constexpr (DICT) {
+                        const int xj = (int)ue[j].x + loff[(int)(ue[j].y & 0xFFu) * 8 + pos];
+                        x[j] = xj < V ? xj : -1;                 // padding: u + kDictPad
+                    } else {
+                        x[j] = split_row<FMT>(rows, rhi, V, W, (int)ue[j].x, pos);
+                    }
+                }
 #pragma unroll
                 for (int j = 0; j < J; ++j) {
                     const int ok = -(int)(((j * R + sub) < kk) & (pos < W));
                     x[j] = (x[j] & ok) | ~ok;
                 }
                 uint64_t m[J];
+                uint32_t pw[J];                    // DICT: the pattern id of x[j]
 #pragma unroll
                 for (int j = 0; j < J; ++j) {
                     const int xi = x[j] & 0x7FFFFFFF;
-                    const uint32_t wv = vis[vsw((xi >> 5) & ((x[j] >> 31) ^ -1))];
+                    const int xs = xi & ((x[j] >> 31) ^ -1);    // padding -> vertex 0
+                    const uint32_t wv = vis[vsw(xs >> 5)];
+                    // the block id beside the visited word, its tuple byte
+                    // right behind (both off the ballot's path: only a push
+                    // uses them)
+                    if (DICT) pw[j] = pat_in(blk_of(xs), xs);
                     m[j] = __ballot((x[j] >= 0) & (((wv >> (xi & 31)) & 1u) == 0u));
                 }
                 // announce the previous push's records now: the LDS reads of
@@ -1463,19 +1554,22 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                 }
                 uint64_t mj = 0;
                 int vv = -1;
+                uint32_t pv = 0;
                 uint2 uj = make_uint2(0u, 0u);
 #pragma unroll
                 for (int j = 0; j < J; ++j)
                     if (j == jstar) {
                         mj = m[j];
                         vv = x[j];
+                        if (DICT) pv = pw[j];
                         uj = ue[j];
                     }
                 const int sstar = (__ffsll((unsigned long long)mj) - 1) / LPR;
                 const int istar = jstar * R + sstar;
                 const uint64_t mm = mj & (lowmask << (sstar * LPR));
                 const int eu = read_lane((int)uj.x, sstar * LPR);
-                const uint32_t ed = WR ? (uint32_t)read_lane((int)uj.y, sstar * LPR) : 0u;
+                const uint32_t ey = YR ? (uint32_t)read_lane((int)uj.y, sstar * LPR) : 0u;
+                const uint32_t ed = DICT ? ey >> 8 : ey;   // the popped entry's depth
                 lsp -= istar + 1;
                 const int cnt = __popcll(mm);
                 // room in the record queue (the writer publishes its progress)
@@ -1516,7 +1610,8 @@ __global__ __launch_bounds__((NS + 1) * 64) void dfs_split_kernel(
                     q[(pub + rank) & (kSplitQ - 1)] =
                         make_uint2((uint32_t)vv | ((uint32_t)pos << 26), (uint32_t)eu);
                     if (HOPS) qd[(pub + rank) & (kSplitQ - 1)] = ed + 1u;
-                    ring[(bot + lsp + rank) & (RING - 1)] = RE::put((uint32_t)vv, ed + 1u);
+                    ring[(bot + lsp + rank) & (RING - 1)] =
+                        RE::put((uint32_t)vv, DICT ? pv | ((ed + 1u) << 8) : ed + 1u);
                 }
                 lsp += cnt;
                 pub += cnt;
@@ -2459,7 +2554,11 @@ static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, in
         return sdnr_fail(SDNR_ERR_INVAL, "dfs split: packed tables need V <= 65535");
     if (tree == kTreeSlot && hops && fmt == kRow32)
         return sdnr_fail(SDNR_ERR_INVAL, "dfs split: slot trees with hop counts need V < 131071");
-    const size_t lds = split_lds_words(V, ring, NS, hops, lpr) * 4;
+    // dictionary rows where the upload built them (rows of <= 8 slots)
+    const bool dict = ctx->dict_bp && lpr == 8 && !kWide;
+    const size_t dict_words =
+        dict ? (size_t)ctx->dict_bpw + 8 * (size_t)ctx->dict_NB + 8 * (size_t)ctx->dict_P : 0;
+    const size_t lds = (split_lds_words(V, ring, NS, hops, lpr, dict) + dict_words) * 4;
     if (lds > SDNR_MAX_LDS_PER_BLOCK)
         return sdnr_fail(SDNR_ERR_INVAL, "graph too large for the LDS visited sets (V=%d)", V);
     size_t bpc = SDNR_LDS_PER_CU / lds;
@@ -2475,11 +2574,12 @@ static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, in
     const void *rows = fmt == kRow32 ? static_cast<const void *>(ctx->ell_col)
                                      : static_cast<const void *>(ctx->ell16);
     int32_t *par = packed ? reinterpret_cast<int32_t *>(d_tree) : d_parent;
-    static const char *names[3][3] = {
+    static const char *names[4][3] = {
         {"dfs_split_kernel<row32>", "dfs_split_kernel<row32>", "dfs_split_kernel<row32,slots>"},
         {"dfs_split_kernel<row16>", "dfs_split_kernel<row16,packed>", "dfs_split_kernel<row16,slots>"},
-        {"dfs_split_kernel<row17>", "dfs_split_kernel<row17>", "dfs_split_kernel<row17,slots>"}};
-    ctx->last_kernel = names[fmt][tree];
+        {"dfs_split_kernel<row17>", "dfs_split_kernel<row17>", "dfs_split_kernel<row17,slots>"},
+        {"dfs_split_kernel<dict>", "dfs_split_kernel<dict,packed>", "dfs_split_kernel<dict,slots>"}};
+    ctx->last_kernel = names[dict ? kRowDict : fmt][tree];
     // rows of 9-16 slots (Jellyfish): search waves issue at raised priority
     // over their writer (measured 1.027 -> 0.973 s on the 100k Jellyfish; the
     // torus rows of 6 slots measured 3 % slower with it, so not there)
@@ -2504,10 +2604,19 @@ static int launch_split_ns(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc, in
         sdnr_allow_lds(reinterpret_cast<const void *>(k), lds);                              \
         hipLaunchKernelGGL(k, dim3(grid), dim3((NS + 1) * 64), lds, ctx->stream, V, W, rows,     \
                            ctx->ell_hi, ctx->ell_port, d_src, nsrc, par, d_port, d_hops,     \
-                           spill, ctx->d_err, flags, wq, nch);                               \
+                           spill, ctx->d_err, flags, wq, nch, ctx->dict_bp, ctx->dict_bt,    \
+                           ctx->dict_off, ctx->dict_bpw, ctx->dict_NB, ctx->dict_P);         \
     } while (0)
 #define SDNR_SPLIT_F(L_, J_, R_, H_)                                                          \
     do {                                                                                     \
+        if constexpr (L_ == 8 && !kWide) {                                                   \
+            if (dict) {                                                                      \
+                if (tree == kTreeSlot) SDNR_SPLIT(L_, J_, R_, H_, kRowDict, kTreeSlot);      \
+                else if (packed) SDNR_SPLIT(L_, J_, R_, H_, kRowDict, kTreePort16);          \
+                else SDNR_SPLIT(L_, J_, R_, H_, kRowDict, kTreeInt32);                       \
+                break;                                                                       \
+            }                                                                                \
+        }                                                                                    \
         if (tree == kTreeSlot) {                                                             \
             if (fmt == kRow16) SDNR_SPLIT(L_, J_, R_, H_, kRow16, kTreeSlot);                \
             else if (fmt == kRow17) SDNR_SPLIT(L_, J_, R_, H_, kRow17, kTreeSlot);           \

@@ -41,6 +41,9 @@ def _strategy(monkeypatch, dfs=None, ell=None):
     if dfs == "global-cumap":                    # split kernel, sources by CU chunk
         monkeypatch.setenv("SDNROUTE_DFS_CUMAP", "1")
         dfs = "global"
+    if dfs == "global-nodict":                   # split kernel on ELL rows, not dictionary rows
+        monkeypatch.setenv("SDNROUTE_DFS_DICT", "0")
+        dfs = "global"
     if dfs:
         monkeypatch.setenv("SDNROUTE_DFS_STRATEGY", dfs)
     if ell is not None:
@@ -71,7 +74,7 @@ def _check_pairs(g, fabric, p, t, srcs):
 
 @pytest.mark.parametrize("strategy", ["auto", "async", "count", "coop", "lds", "global",
                                       "global-ring128", "global-nopack", "global-nosplit",
-                                      "global-cumap"])
+                                      "global-cumap", "global-nodict"])
 @pytest.mark.parametrize("ell", [True, False])
 @pytest.mark.parametrize("name", G.SMALL)
 def test_dfs_small_all_sources(ctx, monkeypatch, name, strategy, ell):
@@ -82,6 +85,49 @@ def test_dfs_small_all_sources(ctx, monkeypatch, name, strategy, ell):
     srcs = np.arange(csr.V, dtype=np.int32)
     p, t = _check_dfs(ctx, csr, srcs)
     _check_pairs(g, fabric, p, t, srcs)
+
+
+@pytest.mark.parametrize("layout", ["int32", "hops", "packed", "slots"])
+@pytest.mark.parametrize("name", ["mock", "fat_tree_k8", "dragonfly_a4_h2_p2", "random_V40",
+                                  "jellyfish_n60_r5", "torus_5x3x2", "torus_4x4x4"])
+def test_dfs_dict_rows_small(ctx, monkeypatch, name, layout):
+    """The split kernel on dictionary rows (row u = u + D[p(u)] from LDS,
+    csrc/capi.hip upload_dict): every small fabric whose rows
+    have <= 8 slots takes it under the split strategy, in every table layout,
+    bit-exact vs the oracle."""
+    _strategy(monkeypatch, "global")
+    csr = G.Golden(name).fabric().csr()
+    if csr.max_degree() > 8:
+        pytest.skip("rows wider than 8 slots: no dictionary rows")
+    srcs = np.arange(csr.V, dtype=np.int32)
+    ctx.upload(csr)
+    po, to, ho = O.dfs_tables(csr, srcs, with_hops=True, nthreads=NTHREADS)
+    if layout in ("int32", "hops"):
+        p, t, h = ctx.dfs_tables(srcs, with_hops=layout == "hops")
+        np.testing.assert_array_equal(p, po)
+        np.testing.assert_array_equal(t, to)
+        if layout == "hops":
+            np.testing.assert_array_equal(h, ho)
+    elif layout == "packed":
+        np.testing.assert_array_equal(ctx.dfs_tables_packed(srcs), _pack(po, to))
+    else:
+        np.testing.assert_array_equal(ctx.dfs_tables_slots(srcs), _expected_slots(csr, po))
+    assert ctx.last_kernel().startswith("dfs_split_kernel<dict"), ctx.last_kernel()
+
+
+def test_dfs_dict_rows_fallback(ctx, monkeypatch):
+    """An irregular fabric with more than 255 distinct row tuples (a random
+    4-regular graph on 600 switches) keeps the ELL rows; the forced-off
+    dictionary (SDNROUTE_DFS_DICT=0) does too; both bit-exact."""
+    _strategy(monkeypatch, "global")
+    csr = T.jellyfish(600, 4, seed=3).csr()
+    srcs = np.arange(0, csr.V, 7, dtype=np.int32)
+    p, t = _check_dfs(ctx, csr, srcs)
+    assert ctx.last_kernel() == "dfs_split_kernel<row16>", ctx.last_kernel()
+    monkeypatch.setenv("SDNROUTE_DFS_DICT", "0")
+    csr = G.Golden("torus_4x4x4").fabric().csr()
+    _check_dfs(ctx, csr, np.arange(csr.V, dtype=np.int32))
+    assert ctx.last_kernel() == "dfs_split_kernel<row16>", ctx.last_kernel()
 
 
 def _pack(p, t):
