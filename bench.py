@@ -302,7 +302,8 @@ def dropin_block(fabric, queries=10000, seed=5):
     return out
 
 
-def materialised_flows(ctx, dev, stream, csr, fabric, srcs, chunk=1 << 24, packed=False):
+def materialised_flows(ctx, dev, stream, csr, fabric, srcs, chunk=1 << 24, packed=False,
+                       overlap=os.environ.get("BENCH_FLOWS_OVERLAP", "1") != "0"):
     """The fdb of EVERY host pair (Router._add_flows_for_path's input,
     reference sdnmpi/router.py:83-104; _route_to_fdb, topology_db.py:127-138)
     materialised in HBM from the default-route tables: the headline counts
@@ -312,7 +313,10 @@ def materialised_flows(ctx, dev, stream, csr, fabric, srcs, chunk=1 << 24, packe
     `chunk` pairs are sized (offsets) and expanded into a reused output
     buffer, timed with HIP events on the kernels' stream.  packed: each entry
     one u32 word, switch | port << 16 (sdnr_route_expand_packed), instead of
-    two int32 arrays."""
+    two int32 arrays.  overlap: chunk c+1's offsets are computed on a second
+    stream (a second library context, two offset buffers) while chunk c is
+    expanded -- the offsets pass (~0.2 ms per chunk) then hides under the
+    entry stores instead of adding to them."""
     V, H = csr.V, fabric.n_hosts
     hv, hp = fabric.host_table()
     S = len(srcs)
@@ -328,11 +332,20 @@ def materialised_flows(ctx, dev, stream, csr, fabric, srcs, chunk=1 << 24, packe
     sw_of_host = torch.from_numpy(hv.astype(np.int32)).to(dev)
     port_of_host = torch.from_numpy(hp.astype(np.int32)).to(dev)
     npairs = H * H
-    off = torch.empty(chunk + 1, dtype=torch.int64, device=dev)
+    offs = [torch.empty(chunk + 1, dtype=torch.int64, device=dev) for _ in range(2)]
+    off = offs[0]
     sw = torch.empty(chunk * max_len, dtype=torch.int32, device=dev)
+    octx, ostream = ctx, stream                  # where the offsets run
+    if overlap:
+        ostream = torch.cuda.Stream(dev)
+        octx = _native.Context(dev.index)
+        octx.upload(csr)
+        octx.set_stream(ostream.cuda_stream)
+    ev_off = [torch.cuda.Event() for _ in range(2)]      # offsets of buffer b written
+    ev_use = [torch.cuda.Event() for _ in range(2)]      # expansion done reading buffer b
     hpo = sw if packed else torch.empty_like(sw)
 
-    def expand(rows, dsts, last, n, same=False):
+    def expand(rows, dsts, last, n, same=False, off=off):
         # same: the tables of the previous chunk -- the walk tables derived
         # from them (packed trees + ancestor tables) are built once per pass
         if packed:
@@ -370,14 +383,27 @@ def materialised_flows(ctx, dev, stream, csr, fabric, srcs, chunk=1 << 24, packe
     e0.record(stream)
     for c, (rows, dsts, last) in enumerate(reqs):
         n = rows.shape[0]
-        ctx.route_offsets_device(hop.data_ptr(), rows.data_ptr(), dsts.data_ptr(), n,
-                                 off.data_ptr(), nrows=S)
-        expand(rows, dsts, last, n, same=c > 0)  # walk tables built in the first chunk
-        entries += off[n]                        # stream-ordered, no host sync
+        b = c % 2
+        if overlap:                              # chunk c's offsets on the second stream,
+            ostream.wait_event(ev_use[b])        # once chunk c-2 no longer reads buffer b
+            if c == 0:
+                ostream.wait_event(e0)
+        octx.route_offsets_device(hop.data_ptr(), rows.data_ptr(), dsts.data_ptr(), n,
+                                  offs[b].data_ptr(), nrows=S)
+        if overlap:
+            ev_off[b].record(ostream)
+            stream.wait_event(ev_off[b])
+        expand(rows, dsts, last, n, same=c > 0, off=offs[b])   # walk tables: first chunk
+        entries += offs[b][n]                    # stream-ordered, no host sync
+        if overlap:
+            ev_use[b].record(stream)             # buffer b read by the expansion and the sum
     e1.record(stream)
     torch.cuda.synchronize(dev)
     wall_ms = (time.perf_counter() - t0) * 1e3
     ctx.synchronize()
+    if overlap:
+        octx.synchronize()
+        octx.close()
     ms = e0.elapsed_time(e1)
     total = int(entries.item())
     # rate from the host clock around the whole loop (synchronised on both
@@ -388,6 +414,7 @@ def materialised_flows(ctx, dev, stream, csr, fabric, srcs, chunk=1 << 24, packe
             "kernel": ctx.last_kernel(), "chunk_pairs": chunk,
             "entry_bytes": 4 if packed else 8,
             "form": "u32 switch | port << 16" if packed else "int32 switch + int32 port",
+            "offsets_overlapped": overlap,
             "note": "flow entries (dpid, out_port) of all %d^2 host pairs written to HBM "
                     "(offsets + output-centric expansion per %d-pair chunk, one reused output "
                     "buffer), tables and requests resident; compare the headline, which "
