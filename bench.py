@@ -98,6 +98,10 @@ def parse():
                          "its GPU idle (k=48), else 1; 1 at N = 1, "
                          "whose line then also reports the same GPU with 3 in flight as "
                          "'pipelined').  Every step still computes and assembles all tables")
+    ap.add_argument("--profile", action="store_true",
+                    help="profiling runs (tools/profile_gpu.sh): only the warmup + timed steps "
+                         "run -- no single-step latency, no extra blocks -- so that a kernel's "
+                         "dispatches per step are its dispatch count / (warmup + steps)")
     ap.add_argument("--rehearse", action="store_true",
                     help="launcher rehearsal on CPU: the N ranks form a gloo group, shard "
                          "the sources and assemble them, and rank 0 prints the line's "
@@ -302,7 +306,8 @@ def dropin_block(fabric, queries=10000, seed=5):
     return out
 
 
-def materialised_flows(ctx, dev, stream, csr, fabric, srcs, chunk=1 << 24, packed=False,
+def materialised_flows(ctx, dev, stream, csr, fabric, srcs,
+                       chunk=int(os.environ.get("BENCH_FLOWS_CHUNK", 1 << 24)), packed=False,
                        overlap=os.environ.get("BENCH_FLOWS_OVERLAP", "1") != "0"):
     """The fdb of EVERY host pair (Router._add_flows_for_path's input,
     reference sdnmpi/router.py:83-104; _route_to_fdb, topology_db.py:127-138)
@@ -1258,10 +1263,10 @@ def main():
         return {"steps_in_flight": k, "ms_per_step": ms, "value": routes / (ms / 1e3),
                 "steps": reps}
 
-    single_ms = single_step_ms()
+    single_ms = None if args.profile else single_step_ms()
     by_inflight = {str(inflight): {"steps_in_flight": inflight, "ms_per_step": ms_per_step,
                                    "value": value, "steps": args.steps, "headline": True}}
-    if inflight > 1:                          # the same ranks, one step at a time
+    if inflight > 1 and not args.profile:     # the same ranks, one step at a time
         by_inflight["1"] = rate_at(1, max(args.steps // 2, 10))
     pipelined = None
     set_bytes = sum(t.numel() * t.element_size() for t in bufs[0])
@@ -1355,7 +1360,7 @@ def main():
         out["multi_gpu"] = multi
         out["config"]["assemble"] = args.assemble
         out["config"]["assemble_reason"] = ASSEMBLE_REASON[args.assemble]
-    if rank == 0 and world == 1 and args.mode == "dfs" and \
+    if rank == 0 and world == 1 and args.mode == "dfs" and not args.profile and \
             float(S) * V * (4 if packed else 8) <= 4e9:
         # the drop-in's host-buffer boundary: sources in, tables out over PCIe
         # (skipped where the host copy of the tables would exceed 4 GB)
@@ -1378,14 +1383,16 @@ def main():
     # fat-trees only: their default routes are ~70 entries; a torus or
     # Jellyfish all-pairs fdb set (~2,400-5,600 entries per pair) is TBs
     if rank == 0 and world == 1 and args.mode == "dfs" and not args.max_sources and \
-            not args.no_flows and not args.all_vertices and args.fabric.startswith("fat_tree"):
+            not args.no_flows and not args.profile and not args.all_vertices and \
+            args.fabric.startswith("fat_tree"):
         # the form the drop-in uses: one u32 word (switch | port << 16) per
         # entry, 4 B; the two int32 arrays (8 B per entry) beside it
         out["materialised_flows"] = materialised_flows(ctx, dev, stream, csr, fabric, srcs,
                                                        packed=True)
         out["materialised_flows_int32"] = materialised_flows(ctx, dev, stream, csr, fabric, srcs)
     if rank == 0 and world == 1 and args.mode == "dfs" and not args.max_sources and \
-            not args.no_flows and not args.all_vertices and args.fabric.startswith("fat_tree"):
+            not args.no_flows and not args.profile and not args.all_vertices and \
+            args.fabric.startswith("fat_tree"):
         out["dropin"] = dropin_block(fabric)
     if world > 1 and not args.no_cpu_baseline and args.mode == "dfs":
         dist.barrier()         # the GPU work of every rank is done: rank 0 alone on the host

@@ -2479,7 +2479,14 @@ static int dfs_batch_depth(const sdnr_ctx *ctx)
 static int dfs_flags(int dflt = 0)
 {
     const char *f = getenv("SDNROUTE_DFS_FLAGS");
-    return f ? atoi(f) : dflt;
+    const int v = f ? atoi(f) : dflt;
+#ifdef SDNR_DIAG_VARIANTS
+    return v;
+#else
+    // the timing diagnostics that leave the tables wrong (no stores, no port
+    // lookups) exist only in the diagnostic build
+    return v & ~(kFlagNoStore | kFlagNoPort);
+#endif
 }
 
 // SDNROUTE_DFS_SPLIT=0 keeps the single-wave lane-packed kernel (A/B, tests)

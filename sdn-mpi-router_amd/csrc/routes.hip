@@ -1090,8 +1090,13 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
             const char *nt = getenv("SDNROUTE_ROUTE_NT");       // "1": non-temporal stores
             // 16-B stores of 4 entries per lane (SDNROUTE_ROUTE_V4=0: 4-B stores)
             const char *v4 = getenv("SDNROUTE_ROUTE_V4");
-            const char *dg = getenv("SDNROUTE_ROUTE_DIAG");   // timing only: 1 no walks, 2 no stores
+#ifdef SDNR_DIAG_VARIANTS
+            // timing only (the entries are then wrong): 1 no walks, 2 no stores
+            const char *dg = getenv("SDNROUTE_ROUTE_DIAG");
             const int diag = dg ? atoi(dg) : 0;
+#else
+            const int diag = 0;                 // never in the product library
+#endif
             // walker / storer waves (route_seg_pipe_kernel): SDNROUTE_ROUTE_PIPE=0
             // keeps the one-role kernel, "W,S,N" picks walkers, storers and
             // slots per walker among the compiled shapes

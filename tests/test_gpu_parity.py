@@ -351,8 +351,9 @@ def test_dfs_fullsize_all_host_sources(ctx, name):
     _check_pairs(g, fabric, p, t, srcs)
 
 
-@pytest.mark.parametrize("split", ["1", "0", "ns3", "ns7", "ns5", "ns5-ring256", "ns11-ring256",
-                                   "cumap0", "cumap1", "j4", "j1"])
+# "1" is the default (CU-chunked sources, NS by shape: 7 on the torus, 5 on
+# the Jellyfish; 8-entry windows); the others force each non-default shape
+@pytest.mark.parametrize("split", ["1", "0", "ns3", "ns11-ring256", "cumap0", "j4"])
 @pytest.mark.parametrize("name,nsample", [("torus_32x32x32_sample", 384),
                                           ("jellyfish_n100000_r16_sample", 48)])
 def test_dfs_fullsize_sampled_sources(ctx, monkeypatch, name, nsample, split):
@@ -757,7 +758,7 @@ def test_shortest_plane_incomplete_words(ctx, monkeypatch, name):
         np.testing.assert_array_equal(nhp, nhpo)
 
 
-@pytest.mark.parametrize("tiles", ["64", "sq128", "64-norelax"])
+@pytest.mark.parametrize("tiles", ["64", "64-norelax"])       # sq128: test_apsp_dragonfly
 def test_apsp_fullsize_k48(ctx, monkeypatch, tiles):
     """k=48 (diameter 4): Bellman-Ford sweeps reach the fixpoint within the
     cap, no squaring pass at all; squaring alone takes 3 passes."""
@@ -1078,7 +1079,7 @@ def test_route_expand_same_tables(ctx, packed):
     run(tabs[1], da, True)
 
 
-@pytest.mark.parametrize("pipe", ["default", "4,4,2", "0"])
+@pytest.mark.parametrize("pipe", ["default", "0"])
 def test_route_expand_k48_large_batch(ctx, monkeypatch, pipe):
     """A 4.3 M-pair batch on k=48 -- the all-pairs order of the materialised
     flows (runs of 24 hosts per destination switch, DFS routes of ~70

@@ -9,8 +9,9 @@ OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 # --inflight 1: no 3-in-flight 'pipelined' launches in the trace (their
-# overlapped durations would mix into the kernel's average)
-BENCH=("$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --inflight 1 "$@")
+# overlapped durations would mix into the kernel's average); --profile: only
+# the 2 warmup + 10 timed steps run (dispatches per step = dispatches / 12)
+BENCH=("$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --inflight 1 --profile "$@")
 stop_if_fatal() { # GPU fault / abort / segfault / timeout -> stop the script
   case $1 in 124|134|137|139) echo "fatal rc=$1 in $2"; exit $1;; esac; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- \

@@ -16,6 +16,12 @@ for n in "$@"; do
     jf_dfs)      run r06_jf_dfs --fabric jellyfish:100000,16,1 --steps 1 --warmup 1 ;;
     flows48)     run r06_flows48 --mode matflows --steps 1 ;;
     apsp48)      run r06_apsp48 --mode apsp ;;
+    dfs48)       run r06_dfs48 --no-flows --layout int32 ;;
+    ecmp48)      run r06_ecmp48 --mode ecmp ;;
+    rflows48)    run r06_rflows48 --mode flows ;;
+    df_sp)       run r06_df_sp --fabric dragonfly:16,8,8 --mode shortest ;;
+    torus_sp)    run r06_torus_sp --fabric torus:32,32,32 --mode shortest --steps 2 --warmup 1 ;;
+    jf_sp)       run r06_jf_sp --fabric jellyfish:100000,16,1 --mode shortest --steps 1 --warmup 1 ;;
     *) echo "unknown profile $n"; exit 2 ;;
   esac
 done
