@@ -382,20 +382,31 @@ __global__ __launch_bounds__(128) void minplus_square64_kernel(int Vp, uint16_t 
 // V^2 x in-degree sweeps, where each squaring pass costs V^3.
 // changed[0]: some block did not reach its fixpoint within cap sweeps;
 // changed[1]: the most sweeps any block ran.
-__global__ __launch_bounds__(1024) void apsp_relax8_kernel(int V, int Vp, int maxd,
+// NQ: u32 words of an in-row that hold entries (in-degree <= 2 NQ), a
+// template so the row loads are whole 16-B loads and the relaxation loop
+// has no branch (a runtime bound put a scalar branch around every load and
+// every LDS read pair: 2.3x slower per sweep)
+template <int NQ>
+__global__ __launch_bounds__(1024) void apsp_relax8_kernel(int V, int Vp,
                                                           const uint16_t *__restrict__ radj,
                                                           uint16_t *__restrict__ D,
                                                           int *__restrict__ changed, int cap)
 {
-    extern __shared__ uint4 L[];                 // L[j] = D[i0..i0+7][j] as 8 u16
+    static_assert(NQ % 4 == 0 && NQ <= 32, "whole 16-B in-row loads");
+    // L[j] = D[i0..i0+7][j] as 8 u16; L[V] = all INF: the in-rows' padding
+    // (sentinel V) relaxes against it to no effect, so the inner loop has no
+    // per-lane branch and its LDS reads issue back to back
+    extern __shared__ uint4 L[];
     const int i0 = blockIdx.x * 8;
-    for (int j = threadIdx.x; j < V; j += blockDim.x) {
+    for (int j = threadIdx.x; j <= V; j += blockDim.x) {
         uint32_t w[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int ra = i0 + 2 * q, rb = ra + 1;
-            const uint32_t a = ra < V ? D[(size_t)ra * Vp + j] : 0xFFFFu;
-            const uint32_t b = rb < V ? D[(size_t)rb * Vp + j] : 0xFFFFu;
+            // rows past V (the last block) hold 0: they never change and
+            // never hold the early exit below back; real rows' L[V] is INF
+            const uint32_t a = ra >= V ? 0u : (j < V ? D[(size_t)ra * Vp + j] : 0xFFFFu);
+            const uint32_t b = rb >= V ? 0u : (j < V ? D[(size_t)rb * Vp + j] : 0xFFFFu);
             w[q] = a | (b << 16);
         }
         L[j] = make_uint4(w[0], w[1], w[2], w[3]);
@@ -407,43 +418,59 @@ __global__ __launch_bounds__(1024) void apsp_relax8_kernel(int V, int Vp, int ma
     while (ch && sweeps < cap) {
         ch = false;
         ++sweeps;
+        u16x2 mx = {0, 0};                      // largest entry this thread saw
         for (int j = threadIdx.x; j < V; j += blockDim.x) {
-            const uint32_t *rr = reinterpret_cast<const uint32_t *>(radj + (size_t)j * 64);
-            uint32_t nb[32];                     // in-row of j, sentinel V
+            const uint4 *rr = reinterpret_cast<const uint4 *>(radj + (size_t)j * 64);
+            uint32_t nb[NQ];                     // in-row of j, sentinel V
 #pragma unroll
-            for (int q = 0; q < 32; ++q) nb[q] = rr[q];
+            for (int q = 0; q < NQ / 4; ++q) {
+                const uint4 t = rr[q];
+                nb[4 * q] = t.x;
+                nb[4 * q + 1] = t.y;
+                nb[4 * q + 2] = t.z;
+                nb[4 * q + 3] = t.w;
+            }
             const uint4 c = L[j];
-            u16x2 cur[4], best[4];
+            u16x2 cur[4], best[4], alt[4];
             cur[0] = __builtin_bit_cast(u16x2, c.x);
             cur[1] = __builtin_bit_cast(u16x2, c.y);
             cur[2] = __builtin_bit_cast(u16x2, c.z);
             cur[3] = __builtin_bit_cast(u16x2, c.w);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) best[r] = cur[r];
+            for (int r = 0; r < 4; ++r) {
+                best[r] = cur[r];
+                alt[r] = cur[r];
+            }
+            // 8 LDS reads in flight per batch (4 in-row words), two
+            // independent min chains (even / odd halves of each word)
 #pragma unroll
-            for (int q = 0; q < 32; ++q) {
-                if (2 * q < maxd) {              // uniform: rows hold <= maxd entries
+            for (int q0 = 0; q0 < NQ; q0 += 4) {
+                uint4 x[8];
 #pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const uint32_t k = h ? nb[q] >> 16 : nb[q] & 0xFFFFu;
-                        if (k < (uint32_t)V) {
-                            const uint4 x = L[k];
-                            best[0] = __builtin_elementwise_min(
-                                best[0], __builtin_elementwise_add_sat(__builtin_bit_cast(u16x2, x.x), one));
-                            best[1] = __builtin_elementwise_min(
-                                best[1], __builtin_elementwise_add_sat(__builtin_bit_cast(u16x2, x.y), one));
-                            best[2] = __builtin_elementwise_min(
-                                best[2], __builtin_elementwise_add_sat(__builtin_bit_cast(u16x2, x.z), one));
-                            best[3] = __builtin_elementwise_min(
-                                best[3], __builtin_elementwise_add_sat(__builtin_bit_cast(u16x2, x.w), one));
-                        }
-                    }
+                for (int t = 0; t < 4; ++t) {
+                    x[2 * t] = L[nb[q0 + t] & 0xFFFFu];
+                    x[2 * t + 1] = L[nb[q0 + t] >> 16];
+                }
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    u16x2 *acc = (t & 1) ? alt : best;
+                    acc[0] = __builtin_elementwise_min(
+                        acc[0], __builtin_elementwise_add_sat(__builtin_bit_cast(u16x2, x[t].x), one));
+                    acc[1] = __builtin_elementwise_min(
+                        acc[1], __builtin_elementwise_add_sat(__builtin_bit_cast(u16x2, x[t].y), one));
+                    acc[2] = __builtin_elementwise_min(
+                        acc[2], __builtin_elementwise_add_sat(__builtin_bit_cast(u16x2, x[t].z), one));
+                    acc[3] = __builtin_elementwise_min(
+                        acc[3], __builtin_elementwise_add_sat(__builtin_bit_cast(u16x2, x[t].w), one));
                 }
             }
             bool d = false;                      // INF + 1 saturates: never below INF
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
+            for (int r = 0; r < 4; ++r) {
+                best[r] = __builtin_elementwise_min(best[r], alt[r]);
                 d |= __builtin_bit_cast(uint32_t, best[r]) != __builtin_bit_cast(uint32_t, cur[r]);
+                mx = __builtin_elementwise_max(mx, best[r]);
+            }
             if (d) {
                 L[j] = make_uint4(__builtin_bit_cast(uint32_t, best[0]),
                                   __builtin_bit_cast(uint32_t, best[1]),
@@ -452,8 +479,16 @@ __global__ __launch_bounds__(1024) void apsp_relax8_kernel(int V, int Vp, int ma
                 ch = true;
             }
         }
+        // exact without a confirming sweep: after s in-place sweeps every
+        // distance <= s + 1 is exact (each sweep extends the exact horizon
+        // by at least one hop), and an entry is an upper bound of its true
+        // distance, so once every entry of the block is finite and <= s + 1
+        // each one equals its true distance
+        const uint32_t m = mx.x > mx.y ? mx.x : mx.y;
+        const bool far = m > (uint32_t)(sweeps + 1);   // INF (0xFFFF) included
         ch = __syncthreads_or(ch);
         any |= ch;
+        if (!__syncthreads_or(far)) ch = false;
     }
     if (any) {                                   // write the improved rows back
         for (int j = threadIdx.x; j < V; j += blockDim.x) {
@@ -494,8 +529,9 @@ static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp, int m
     // distance <= 2^s) the largest finite distance M is < 2^s.
     const int nt = Vp / mt;
     const char *rf = getenv("SDNROUTE_APSP_RELAX");
-    // the transposed 8-row block must fit LDS (16 B per vertex: V <= 10,240)
-    const bool relax = ctx->radj16 && ctx->max_indeg <= 64 && (size_t)V * 16 <= 160 * 1024 &&
+    // the transposed 8-row block must fit LDS (16 B per vertex + the INF
+    // column: V < 10,240)
+    const bool relax = ctx->radj16 && ctx->max_indeg <= 64 && ((size_t)V + 1) * 16 <= 160 * 1024 &&
                        !(rf && !strcmp(rf, "0"));
     // sweeps per squaring pass of cost: V^3 / (V E) = V / avg degree, /4
     // for the sweeps' lower op rate (measured k=48: 46 us per sweep of all
@@ -504,13 +540,20 @@ static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp, int m
     const int cap = capl < 4 ? 4 : (capl > 64 ? 64 : (int)capl);
     ctx->last_launches = 0;
     ctx->last_sweeps = 0;
-    if (relax) sdnr_allow_lds(reinterpret_cast<const void *>(apsp_relax8_kernel), (size_t)V * 16);
+    // in-row words per column, rounded to whole 16-B loads
+    const int nq = ((ctx->max_indeg + 1) / 2 + 3) & ~3;
+    auto relax_kernel = nq <= 4 ? apsp_relax8_kernel<4>
+                      : nq <= 8 ? apsp_relax8_kernel<8>
+                      : nq <= 12 ? apsp_relax8_kernel<12>
+                      : nq <= 16 ? apsp_relax8_kernel<16>
+                      : nq <= 24 ? apsp_relax8_kernel<24> : apsp_relax8_kernel<32>;
+    if (relax) sdnr_allow_lds(reinterpret_cast<const void *>(relax_kernel), ((size_t)V + 1) * 16);
     for (int it = 1; it <= 40; ++it) {         // 2^40 >> any hop distance
         if (relax) {
             SDNR_HIP(hipMemsetAsync(changed, 0, 2 * sizeof(int), ctx->stream));
-            hipLaunchKernelGGL(apsp_relax8_kernel, dim3((V + 7) / 8), dim3(1024),
-                               (size_t)V * 16, ctx->stream, V, Vp, ctx->max_indeg, ctx->radj16,
-                               D, changed, cap);
+            hipLaunchKernelGGL(relax_kernel, dim3((V + 7) / 8), dim3(1024),
+                               ((size_t)V + 1) * 16, ctx->stream, V, Vp, ctx->radj16, D, changed,
+                               cap);
             SDNR_HIP(hipGetLastError());
             int h[2] = {1, 0};
             int rc = sdnr_fetch_ints(ctx, changed, 2, h);
