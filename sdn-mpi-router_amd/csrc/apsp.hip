@@ -389,8 +389,10 @@ __global__ __launch_bounds__(128) void minplus_square64_kernel(int Vp, uint16_t 
 template <int NQ>
 __global__ __launch_bounds__(1024) void apsp_relax8_kernel(int V, int Vp,
                                                           const uint16_t *__restrict__ radj,
+                                                          const uint16_t *__restrict__ adj,
                                                           uint16_t *__restrict__ D,
-                                                          int *__restrict__ changed, int cap)
+                                                          int *__restrict__ changed, int cap,
+                                                          int fresh)
 {
     static_assert(NQ % 4 == 0 && NQ <= 32, "whole 16-B in-row loads");
     // L[j] = D[i0..i0+7][j] as 8 u16; L[V] = all INF: the in-rows' padding
@@ -398,7 +400,33 @@ __global__ __launch_bounds__(1024) void apsp_relax8_kernel(int V, int Vp,
     // per-lane branch and its LDS reads issue back to back
     extern __shared__ uint4 L[];
     const int i0 = blockIdx.x * 8;
-    for (int j = threadIdx.x; j <= V; j += blockDim.x) {
+    if (fresh) {
+        // D not initialised: the block's 8 rows start as 0 on the diagonal,
+        // 1 on each out-link (the rows' u16 out-rows, 64 lanes per row), INF
+        // elsewhere -- what apsp_init_kernel + apsp_edges_kernel write, built
+        // here in LDS instead of 2 x V^2 x 2 bytes through HBM
+        uint16_t *L16 = reinterpret_cast<uint16_t *>(L);
+        for (int j = threadIdx.x; j <= V; j += blockDim.x) {
+            uint32_t w[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int ra = i0 + 2 * q, rb = ra + 1;
+                const uint32_t a = ra >= V ? 0u : (ra == j ? 0u : 0xFFFFu);
+                const uint32_t b = rb >= V ? 0u : (rb == j ? 0u : 0xFFFFu);
+                w[q] = a | (b << 16);
+            }
+            L[j] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < 8 * 64; t += blockDim.x) {
+            const int r = t >> 6, i = i0 + r;
+            if (i < V) {
+                const int x = (int)adj[(size_t)i * 64 + (t & 63)];
+                if (x < V && x != i) L16[(size_t)x * 8 + r] = 1;
+            }
+        }
+    }
+    for (int j = threadIdx.x; j <= V && !fresh; j += blockDim.x) {
         uint32_t w[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -490,7 +518,7 @@ __global__ __launch_bounds__(1024) void apsp_relax8_kernel(int V, int Vp,
         any |= ch;
         if (!__syncthreads_or(far)) ch = false;
     }
-    if (any) {                                   // write the improved rows back
+    if (any || fresh) {                          // write the improved (or new) rows back
         for (int j = threadIdx.x; j < V; j += blockDim.x) {
             const uint4 c = L[j];
             const uint32_t w[4] = {c.x, c.y, c.z, c.w};
@@ -515,10 +543,6 @@ static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp, int m
     int rc = sdnr_reserve(&ctx->scratch2, &ctx->scratch2_bytes, 256);
     if (rc) return rc;
     int *changed = static_cast<int *>(ctx->scratch2);
-    hipLaunchKernelGGL(apsp_init_kernel, dim3(1024), dim3(256), 0, ctx->stream, V, Vp,
-                       ctx->row_ptr, ctx->col, D);
-    hipLaunchKernelGGL(apsp_edges_kernel, dim3((V + 255) / 256), dim3(256), 0, ctx->stream, V, Vp,
-                       ctx->row_ptr, ctx->col, D);
     // Squaring passes double the exact horizon for V^3 each; Bellman-Ford
     // sweeps (apsp_relax8_kernel) extend it by one hop for V^2 x in-degree
     // each and stop by themselves at the fixpoint.  So: sweep to the
@@ -548,12 +572,22 @@ static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp, int m
                       : nq <= 16 ? apsp_relax8_kernel<16>
                       : nq <= 24 ? apsp_relax8_kernel<24> : apsp_relax8_kernel<32>;
     if (relax) sdnr_allow_lds(reinterpret_cast<const void *>(relax_kernel), ((size_t)V + 1) * 16);
+    // the first sweep launch builds its rows from the out-rows itself (no
+    // init / edge passes over V^2); the padding of a Vp > V matrix, which
+    // the squaring passes read, still comes from the init pass
+    const bool fused = relax && ctx->adj16;
+    if (!fused || Vp != V)
+        hipLaunchKernelGGL(apsp_init_kernel, dim3(1024), dim3(256), 0, ctx->stream, V, Vp,
+                           ctx->row_ptr, ctx->col, D);
+    if (!fused)
+        hipLaunchKernelGGL(apsp_edges_kernel, dim3((V + 255) / 256), dim3(256), 0, ctx->stream,
+                           V, Vp, ctx->row_ptr, ctx->col, D);
     for (int it = 1; it <= 40; ++it) {         // 2^40 >> any hop distance
         if (relax) {
             SDNR_HIP(hipMemsetAsync(changed, 0, 2 * sizeof(int), ctx->stream));
             hipLaunchKernelGGL(relax_kernel, dim3((V + 7) / 8), dim3(1024),
-                               ((size_t)V + 1) * 16, ctx->stream, V, Vp, ctx->radj16, D, changed,
-                               cap);
+                               ((size_t)V + 1) * 16, ctx->stream, V, Vp, ctx->radj16, ctx->adj16,
+                               D, changed, cap, (int)(fused && it == 1));
             SDNR_HIP(hipGetLastError());
             int h[2] = {1, 0};
             int rc = sdnr_fetch_ints(ctx, changed, 2, h);
