@@ -382,6 +382,12 @@ __global__ __launch_bounds__(128) void minplus_square64_kernel(int Vp, uint16_t 
 // V^2 x in-degree sweeps, where each squaring pass costs V^3.
 // changed[0]: some block did not reach its fixpoint within cap sweeps;
 // changed[1]: the most sweeps any block ran.
+// column k's 16-B entry lives at lsw(k): the 16 entries of each aligned
+// group of 16 (one 256-B LDS bank row) permuted by the group number, so
+// columns a multiple of 16 apart -- a fat-tree aggregation switch's core
+// neighbours are 24 apart -- fall in different bank slots of a ds_read_b128
+__device__ __forceinline__ int lsw(int k) { return k ^ ((k >> 4) & 15); }
+
 // NQ: u32 words of an in-row that hold entries (in-degree <= 2 NQ), a
 // template so the row loads are whole 16-B loads and the relaxation loop
 // has no branch (a runtime bound put a scalar branch around every load and
@@ -415,14 +421,14 @@ __global__ __launch_bounds__(1024) void apsp_relax8_kernel(int V, int Vp,
                 const uint32_t b = rb >= V ? 0u : (rb == j ? 0u : 0xFFFFu);
                 w[q] = a | (b << 16);
             }
-            L[j] = make_uint4(w[0], w[1], w[2], w[3]);
+            L[lsw(j)] = make_uint4(w[0], w[1], w[2], w[3]);
         }
         __syncthreads();
         for (int t = threadIdx.x; t < 8 * 64; t += blockDim.x) {
             const int r = t >> 6, i = i0 + r;
             if (i < V) {
                 const int x = (int)adj[(size_t)i * 64 + (t & 63)];
-                if (x < V && x != i) L16[(size_t)x * 8 + r] = 1;
+                if (x < V && x != i) L16[(size_t)lsw(x) * 8 + r] = 1;
             }
         }
     }
@@ -437,7 +443,7 @@ __global__ __launch_bounds__(1024) void apsp_relax8_kernel(int V, int Vp,
             const uint32_t b = rb >= V ? 0u : (j < V ? D[(size_t)rb * Vp + j] : 0xFFFFu);
             w[q] = a | (b << 16);
         }
-        L[j] = make_uint4(w[0], w[1], w[2], w[3]);
+        L[lsw(j)] = make_uint4(w[0], w[1], w[2], w[3]);
     }
     __syncthreads();
     const u16x2 one = {1, 1};
@@ -458,7 +464,7 @@ __global__ __launch_bounds__(1024) void apsp_relax8_kernel(int V, int Vp,
                 nb[4 * q + 2] = t.z;
                 nb[4 * q + 3] = t.w;
             }
-            const uint4 c = L[j];
+            const uint4 c = L[lsw(j)];
             u16x2 cur[4], best[4], alt[4];
             cur[0] = __builtin_bit_cast(u16x2, c.x);
             cur[1] = __builtin_bit_cast(u16x2, c.y);
@@ -476,8 +482,8 @@ __global__ __launch_bounds__(1024) void apsp_relax8_kernel(int V, int Vp,
                 uint4 x[8];
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                    x[2 * t] = L[nb[q0 + t] & 0xFFFFu];
-                    x[2 * t + 1] = L[nb[q0 + t] >> 16];
+                    x[2 * t] = L[lsw((int)(nb[q0 + t] & 0xFFFFu))];
+                    x[2 * t + 1] = L[lsw((int)(nb[q0 + t] >> 16))];
                 }
 #pragma unroll
                 for (int t = 0; t < 8; ++t) {
@@ -500,7 +506,7 @@ __global__ __launch_bounds__(1024) void apsp_relax8_kernel(int V, int Vp,
                 mx = __builtin_elementwise_max(mx, best[r]);
             }
             if (d) {
-                L[j] = make_uint4(__builtin_bit_cast(uint32_t, best[0]),
+                L[lsw(j)] = make_uint4(__builtin_bit_cast(uint32_t, best[0]),
                                   __builtin_bit_cast(uint32_t, best[1]),
                                   __builtin_bit_cast(uint32_t, best[2]),
                                   __builtin_bit_cast(uint32_t, best[3]));
@@ -520,7 +526,7 @@ __global__ __launch_bounds__(1024) void apsp_relax8_kernel(int V, int Vp,
     }
     if (any || fresh) {                          // write the improved (or new) rows back
         for (int j = threadIdx.x; j < V; j += blockDim.x) {
-            const uint4 c = L[j];
+            const uint4 c = L[lsw(j)];
             const uint32_t w[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -555,7 +561,8 @@ static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp, int m
     const char *rf = getenv("SDNROUTE_APSP_RELAX");
     // the transposed 8-row block must fit LDS (16 B per vertex + the INF
     // column: V < 10,240)
-    const bool relax = ctx->radj16 && ctx->max_indeg <= 64 && ((size_t)V + 1) * 16 <= 160 * 1024 &&
+    const bool relax = ctx->radj16 && ctx->max_indeg <= 64 &&
+                       (((size_t)V + 1 + 15) & ~(size_t)15) * 16 <= 160 * 1024 &&
                        !(rf && !strcmp(rf, "0"));
     // sweeps per squaring pass of cost: V^3 / (V E) = V / avg degree, /4
     // for the sweeps' lower op rate (measured k=48: 46 us per sweep of all
@@ -571,7 +578,9 @@ static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp, int m
                       : nq <= 12 ? apsp_relax8_kernel<12>
                       : nq <= 16 ? apsp_relax8_kernel<16>
                       : nq <= 24 ? apsp_relax8_kernel<24> : apsp_relax8_kernel<32>;
-    if (relax) sdnr_allow_lds(reinterpret_cast<const void *>(relax_kernel), ((size_t)V + 1) * 16);
+    // V + 1 entries (the INF column), whole groups of 16 (the swizzle lsw)
+    const size_t lbytes = (((size_t)V + 1 + 15) & ~(size_t)15) * 16;
+    if (relax) sdnr_allow_lds(reinterpret_cast<const void *>(relax_kernel), lbytes);
     // the first sweep launch builds its rows from the out-rows itself (no
     // init / edge passes over V^2); the padding of a Vp > V matrix, which
     // the squaring passes read, still comes from the init pass
@@ -585,9 +594,9 @@ static int launch_apsp_squaring(sdnr_ctx *ctx, uint16_t *D, int V, int Vp, int m
     for (int it = 1; it <= 40; ++it) {         // 2^40 >> any hop distance
         if (relax) {
             SDNR_HIP(hipMemsetAsync(changed, 0, 2 * sizeof(int), ctx->stream));
-            hipLaunchKernelGGL(relax_kernel, dim3((V + 7) / 8), dim3(1024),
-                               ((size_t)V + 1) * 16, ctx->stream, V, Vp, ctx->radj16, ctx->adj16,
-                               D, changed, cap, (int)(fused && it == 1));
+            hipLaunchKernelGGL(relax_kernel, dim3((V + 7) / 8), dim3(1024), lbytes, ctx->stream,
+                               V, Vp, ctx->radj16, ctx->adj16, D, changed, cap,
+                               (int)(fused && it == 1));
             SDNR_HIP(hipGetLastError());
             int h[2] = {1, 0};
             int rc = sdnr_fetch_ints(ctx, changed, 2, h);
