@@ -3,6 +3,7 @@ self-check histograms), dict -> CSR export == the generators' direct CSR,
 CSR conventions (ascending dpid order, sorted rows, last-write-wins parallel
 links), and fdb expansion helpers."""
 import collections
+import os
 
 import numpy as np
 import pytest
@@ -173,3 +174,29 @@ def test_pool_failed_fill_leaves_slots_blank():
     assert all((a[rows] == 5).all() for a in pool.arrays)
     others = [i for i in range(pool.size) if i not in rows]
     assert all((a[others] == -1).all() for a in pool.arrays)
+
+
+def test_profile_coalescing_figures():
+    """tools/summarize_profile.py's read-coalescing figures:
+    tag lookups per VMEM instruction (4 = one line per quarter-wave, the
+    floor), L2 requests per load, L1 hit rate -- from per-dispatch counter
+    means, here the round-6 headline kernel's own (profiles/r06_dfs48p)."""
+    import importlib.util
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location(
+        "summarize_profile", os.path.join(root, "tools", "summarize_profile.py"))
+    sp = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sp)
+    c = {"TCP_TOTAL_CACHE_ACCESSES_sum": 400.0, "SQ_INSTS_VMEM_RD": 90.0,
+         "SQ_INSTS_VMEM_WR": 10.0, "TCP_TCC_READ_REQ_sum": 45.0, "TCP_TOTAL_READ_sum": 900.0}
+    co = sp.coalescing(c)
+    assert co["tag_lookups_per_vmem"] == 4.0
+    assert co["l2_req_per_vmem_rd"] == 0.5
+    assert abs(co["l1_read_hit"] - 0.95) < 1e-12
+    assert sp.coalescing({}) == {}
+    pmc = json.load(open(os.path.join(root, "profiles", "r06_dfs48p_pmc.json")))
+    k = [n for n in pmc if "dfs_async_kernel" in n][0]
+    got = sp.coalescing(pmc[k]["counters"])
+    assert 4.0 <= got["tag_lookups_per_vmem"] < 4.5        # coalesced: ~one line per quarter-wave
+    assert got["l1_read_hit"] > 0.9

@@ -35,7 +35,11 @@ for nw in [int(x) for x in os.environ.get("STAMPS_WAVES", "3,4,5").split(",")]:
     os.environ["SDNROUTE_DFS_ASYNC_WAVES"] = str(nw)
     for rep in range(2):
         L.sdnr_debug_stamps(buf)
-        ctx.dfs_tables_device(ts.data_ptr(), len(srcs), p.data_ptr(), t.data_ptr(), timing=True)
+        if os.environ.get("STAMPS_PACKED") == "1":      # the headline's packed tables
+            ctx.dfs_tables_packed_device(ts.data_ptr(), len(srcs), p.data_ptr(), timing=True)
+        else:
+            ctx.dfs_tables_device(ts.data_ptr(), len(srcs), p.data_ptr(), t.data_ptr(),
+                                  timing=True)
         ms = ctx.last_kernel_ms()
         ctx.synchronize()
         L.sdnr_debug_stamps(buf)
