@@ -618,7 +618,7 @@ static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *
             // rows of <= 32 in-neighbours: lanes 32..63 repeat lanes 0..31 (the
             // dummies stay per lane), so a worker pairs two children per load
             const bool pair = maxin <= SDNR_WAVE / 2;
-            const char *pe = getenv("SDNROUTE_DFS_PAIR");          // 0: off (A/B)
+            const char *pe = sdnr_tune_env("SDNROUTE_DFS_PAIR");          // 0: off (A/B)
             ctx->radj_pair = pair && !(pe && !strcmp(pe, "0"));
             auto at = [&](size_t i) {
                 return ctx->radj_pair ? (i & ~(size_t)(SDNR_WAVE / 2)) : i;   // lane l -> l & 31

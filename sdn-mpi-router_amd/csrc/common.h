@@ -3,6 +3,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <stddef.h>
 
@@ -143,6 +144,20 @@ inline void sdnr_allow_lds(const void *fn, size_t bytes)
 // bounded waits that ran out, and 32 for the split kernel's CU-numbering spin,
 // split_cu_number); sdnr_synchronize turns a nonzero word into an error, the
 // specific INVAL causes below tested bit by bit (a word may hold several)
+// A/B tuning knobs that only select non-default shapes (worker widths,
+// block shapes, store hints): read by the diagnostic build alone
+// (tools/diag/build_diag.sh, -DSDNR_DIAG_VARIANTS); the product library
+// always takes its measured defaults (knob sprawl)
+inline const char *sdnr_tune_env(const char *name)
+{
+#ifdef SDNR_DIAG_VARIANTS
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
 constexpr int kDictPad = 0x40000000;   // dictionary-row padding offset (u + pad >= V)
 constexpr int kDictMaxP = 255;         // pattern ids are bytes
 constexpr int kErrLastPort = 256;   // sdnr_route_expand_packed: a last port outside [0, 0xFFFF]

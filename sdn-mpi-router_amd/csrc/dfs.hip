@@ -2298,7 +2298,7 @@ static int packed_ring(int V, int W)
 // SDNROUTE_DFS_PACKED_J overrides
 static int packed_j8(int V)
 {
-    if (const char *f = getenv("SDNROUTE_DFS_PACKED_J")) {
+    if (const char *f = sdnr_tune_env("SDNROUTE_DFS_PACKED_J")) {
         const int j = atoi(f);
         if (j == 1 || j == 2) return j;
     }
@@ -2411,7 +2411,7 @@ void launch_coop(int kw, int grid, size_t lds, hipStream_t st, int V, const uint
 // slots per wave of the cooperative kernel (4 waves): SDNROUTE_DFS_COOP_KW
 static int dfs_coop_kw()
 {
-    if (const char *f = getenv("SDNROUTE_DFS_COOP_KW")) {
+    if (const char *f = sdnr_tune_env("SDNROUTE_DFS_COOP_KW")) {
         const int k = atoi(f);
         if (k == 2 || k == 4 || k == 8) return k;
     }
@@ -2456,7 +2456,7 @@ static int dfs_async_waves(const sdnr_ctx *ctx, int nsrc)
 // waves per source of the counted-pop kernel: SDNROUTE_DFS_COUNT_WAVES=2|4|6
 static int dfs_count_waves()
 {
-    if (const char *f = getenv("SDNROUTE_DFS_COUNT_WAVES")) {
+    if (const char *f = sdnr_tune_env("SDNROUTE_DFS_COUNT_WAVES")) {
         const int k = atoi(f);
         if (k == 2 || k == 4 || k == 6) return k;
     }
@@ -2474,7 +2474,7 @@ static bool packed_ok()
 // deeper; SDNROUTE_DFS_BATCH=1|4|8|16 overrides (tuning / tests)
 static int dfs_batch_depth(const sdnr_ctx *ctx)
 {
-    if (const char *f = getenv("SDNROUTE_DFS_BATCH")) {
+    if (const char *f = sdnr_tune_env("SDNROUTE_DFS_BATCH")) {
         const int k = atoi(f);
         if (k == 1 || k == 4 || k == 8 || k == 16) return k;
     }
@@ -2483,7 +2483,7 @@ static int dfs_batch_depth(const sdnr_ctx *ctx)
 
 static int dfs_flags(int dflt = 0)
 {
-    const char *f = getenv("SDNROUTE_DFS_FLAGS");
+    const char *f = sdnr_tune_env("SDNROUTE_DFS_FLAGS");
     const int v = f ? atoi(f) : dflt;
 #ifdef SDNR_DIAG_VARIANTS
     return v;
@@ -2868,7 +2868,7 @@ int sdnr_launch_dfs(sdnr_ctx *ctx, const int32_t *d_src, int32_t nsrc,
         // 1,152-source headline they measured 0.0895 -> 0.1010 ms, so the
         // u16 rows stay there (SDNROUTE_DFS_DW=0|1 forces either)
         const bool pair = preswz && ctx->radj_pair;
-        const char *dq = getenv("SDNROUTE_DFS_DW");
+        const char *dq = sdnr_tune_env("SDNROUTE_DFS_DW");
         bool dw = preswz && !pair && !c16 && nw >= 6;
         if (dq) dw = preswz && !pair && !c16 && !strcmp(dq, "1");
         int cgrid = (int)((size_t)ctx->num_cus * cpc);

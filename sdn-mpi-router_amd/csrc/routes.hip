@@ -1085,9 +1085,9 @@ int sdnr_launch_route_expand(sdnr_ctx *ctx, const int32_t *d_parent, const int32
             // 4 waves per workgroup, one 64-pair group per wave at a time
             int64_t g = (((int64_t)npairs + 63) / 64 + 3) / 4;
             int wpc = 8;                                  // workgroups per CU
-            if (const char *gf = getenv("SDNROUTE_ROUTE_WGS")) wpc = atoi(gf) > 0 ? atoi(gf) : 8;
+            if (const char *gf = sdnr_tune_env("SDNROUTE_ROUTE_WGS")) wpc = atoi(gf) > 0 ? atoi(gf) : 8;
             if (g > ctx->num_cus * wpc) g = ctx->num_cus * wpc;
-            const char *nt = getenv("SDNROUTE_ROUTE_NT");       // "1": non-temporal stores
+            const char *nt = sdnr_tune_env("SDNROUTE_ROUTE_NT");       // "1": non-temporal stores
             // 16-B stores of 4 entries per lane (SDNROUTE_ROUTE_V4=0: 4-B stores)
             const char *v4 = getenv("SDNROUTE_ROUTE_V4");
 #ifdef SDNR_DIAG_VARIANTS

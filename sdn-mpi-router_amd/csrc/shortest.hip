@@ -1162,7 +1162,7 @@ static int launch_sp_apsp(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, uin
 // (SDNROUTE_SP_APSP=0|1 overrides the measured rule)
 static bool sp_apsp_default(const sdnr_ctx *ctx, int32_t ndst)
 {
-    if (const char *f = getenv("SDNROUTE_SP_APSP")) return !strcmp(f, "1");
+    if (const char *f = sdnr_tune_env("SDNROUTE_SP_APSP")) return !strcmp(f, "1");
     (void)ctx;
     (void)ndst;
     return false;
@@ -1256,12 +1256,12 @@ static int launch_plane_dp(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst, ui
     // destination set): 64-vertex blocks, so every CU gets work
     // (SDNROUTE_PLANE_BLOCK=256|64 overrides)
     bool small = (size_t)gx * nbatch < 2 * (size_t)ctx->num_cus;
-    if (const char *f = getenv("SDNROUTE_PLANE_BLOCK")) small = atoi(f) == 64;
+    if (const char *f = sdnr_tune_env("SDNROUTE_PLANE_BLOCK")) small = atoi(f) == 64;
     const int lb = small ? 64 : 256;
     // level pass: batches per block on small graphs (SDNROUTE_PLANE_BPB=2|4;
     // 4 measured k=48 0.0917 -> 0.0926 ms, dragonfly 0.0625 -> 0.0608 ms)
     int bpb = 1;
-    if (const char *f = getenv("SDNROUTE_PLANE_BPB")) {
+    if (const char *f = sdnr_tune_env("SDNROUTE_PLANE_BPB")) {
         const int k = atoi(f);
         if (small && (k == 1 || k == 2 || k == 4)) bpb = k;
     }
@@ -1443,7 +1443,7 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
         if (grid > ndst) grid = ndst;
         // SDNROUTE_SP_VARIANT: 0 = 4 waves x 16 rows in flight (default),
         // 1 = 4 x 8, 2 = 8 x 8 (tuning)
-        const char *vf = getenv("SDNROUTE_SP_VARIANT");
+        const char *vf = sdnr_tune_env("SDNROUTE_SP_VARIANT");
         const int var = vf ? atoi(vf) : 0;
         static const char *names[2][3] = {
             {"bfs_dest_kernel<4,16,asym>", "bfs_dest_kernel<4,8,asym>", "bfs_dest_kernel<8,8,asym>"},
@@ -1493,7 +1493,7 @@ int sdnr_launch_shortest(sdnr_ctx *ctx, const int32_t *d_dst, int32_t ndst,
         ctx->last_kernel = names[sym ? 1 : 0][li];
         // SDNROUTE_SP_LANES_G=1|2|4|8: frontier groups in flight per wave
         // (tuning; torus 32^3: 1 24.6 ms, 2 22.5 ms, 4 24.4 ms, 8 29.6 ms)
-        const char *gf = getenv("SDNROUTE_SP_LANES_G");
+        const char *gf = sdnr_tune_env("SDNROUTE_SP_LANES_G");
         const int gsel = gf ? atoi(gf) : 2;
 #define SDNR_BFS_LANES_G(LPR_, S_, G_)                                                       \
     do {                                                                                     \
