@@ -171,3 +171,60 @@ def test_rccl_all_gather_table_dtypes():
     res = q.get(timeout=240)
     p.join(60)
     assert res == [True, True, True, True], res
+
+
+def _check_worker(rank, world, port, broken, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "sdn-mpi-router_amd")]
+    from sdnmpi_amd import distributed as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        if broken == "root":                # every rank's root-gather raises
+            def boom(*a, **k):
+                raise RuntimeError("p2p unavailable")
+            D.gather_rows_to_root = boom
+        elif broken == "wrong":             # the all-gather returns wrong rows on rank 1
+            real = D.all_gather_rows_async
+
+            def bad(local, out, group=None):
+                w = real(local, out, group)
+                w.wait()
+                if dist.get_rank() == 1:
+                    out.zero_()
+                return w
+            D.all_gather_rows_async = bad
+        res = D.check_assembly()
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("broken", ["none", "root", "wrong"])
+def test_check_assembly_preflight(broken):
+    """distributed.check_assembly, the preflight bench.py runs before an
+    N > 1 line: both forms ok on a healthy group; a form that raises is
+    reported as an error on every rank; wrong rows seen by ANY rank are
+    reported on every rank (the verdict is all-reduced), so all ranks take
+    the same fallback decision."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_check_worker, args=(r, world, port, broken, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for r in range(world):
+        res = got[r]
+        if broken == "none":
+            assert res == {"root": "ok", "all": "ok"}
+        elif broken == "root":
+            assert res["root"].startswith("error") and res["all"] == "ok"
+        else:
+            assert res["root"] == "ok" and res["all"] == "wrong rows assembled"
