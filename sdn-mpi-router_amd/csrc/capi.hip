@@ -390,7 +390,7 @@ static int graph_upload_one(sdnr_ctx *ctx, int32_t V, int32_t E, const int32_t *
 // dictionary level: blocks of 32 consecutive switches as tuples of 32
 // pattern bytes (a 32^3 torus: 9 distinct x-lines), so a switch's pattern is
 // bt[bp[u >> 5]][u & 31] and the whole form -- V / 32 block bytes, the block
-// tuples and D -- takes ~1.4 KB of LDS for the 32^3 torus (a flat byte per
+// tuples and D -- takes 2.2 KB of LDS for the 32^3 torus (a flat byte per
 // switch, 32 KB, halved the workgroups per CU and measured slower: 99.5 vs
 // 86.6 ms).  Then a DFS window reads no row from L2.  Built when V <= 65535,
 // rows have <= 8 slots and both levels have <= kDictMaxP entries (else the
