@@ -401,6 +401,17 @@ __device__ __forceinline__ int wave_incl_scan(int x)
     return x;
 }
 
+// Entries a run stores one by one before its 16-B body: up to the next
+// 128-B line of the output when both arrays share the line phase (the u32
+// form: one array), else up to the next 16 B.  A body that starts on a line
+// makes every full wave of 16-B stores cover 8 whole lines instead of 9
+// partial ones (store probe)
+__device__ __forceinline__ int store_head(const uint32_t *o, const uint32_t *op, int total)
+{
+    const uint32_t m = (op == nullptr || ((((uintptr_t)o ^ (uintptr_t)op) & 127u) == 0)) ? 127u : 15u;
+    return min(total, (int)((((m + 1u) - ((uint32_t)(uintptr_t)o & m)) & m) >> 2));
+}
+
 // Output-centric expansion (the default for packed trees).  Consecutive
 // pairs very often ask for the same (tree row, destination switch) -- every
 // host on a switch has the same route from a given source switch, and the
@@ -417,7 +428,7 @@ __device__ __forceinline__ int wave_incl_scan(int x)
 // OUTP: entries as one u32 each, switch | port << 16 (the tree word layout:
 // the LDS buffer is copied as is) instead of two int32 arrays.  V4: a run's
 // entries go out as 16-B stores, 4 consecutive entries per lane (per array),
-// after a head of up to 3 single entries to the 16-B boundary
+// after a head of single entries to the line (or 16-B) boundary (store_head)
 template <int CAP, bool NT, bool OUTP, bool V4 = false>
 __global__ __launch_bounds__(256) void route_seg_packed_kernel(
     int V, const uint32_t *__restrict__ tree, Anc16 anc,
@@ -585,7 +596,7 @@ __global__ __launch_bounds__(256) void route_seg_packed_kernel(
                             op[t] = pt_of(q, k);
                         }
                     };
-                    const int head = min(total, (int)(((16u - ((uint32_t)(uintptr_t)o & 15u)) & 15u) >> 2));
+                    const int head = store_head(o, op, total);
                     if (lane < head) {
                         int q, k;
                         qk(lane, q, k);
@@ -897,7 +908,7 @@ __global__ __launch_bounds__((NWK + NST) * 64) void route_seg_pipe_kernel(
                 const bool v4 = total >= 256 &&
                                 (OUTP || ((((uintptr_t)o ^ (uintptr_t)op) & 15u) == 0));
                 if (v4) {
-                    const int hd = min(total, (int)(((16u - ((uint32_t)(uintptr_t)o & 15u)) & 15u) >> 2));
+                    const int hd = store_head(o, op, total);
                     if (lane < hd) put1(lane);
                     const int bend = hd + ((total - hd) & ~3);
                     for (int t0 = hd; t0 < bend; t0 += 256) {

@@ -1143,6 +1143,90 @@ def test_route_expand_k48_large_batch(ctx, monkeypatch, pipe):
         np.testing.assert_array_equal(e[o[i]:o[i + 1]] >> 16, shp[so[j]:so[j + 1]])
 
 
+@pytest.mark.parametrize("fab", ["fat_tree:48", "torus:16,16,16"])
+def test_route_expand_pipe_edges(ctx, monkeypatch, fab):
+    """route_seg_pipe_kernel (walker / storer waves, line-aligned store
+    heads) on a request stream that puts every kind of pair next to slot and
+    group boundaries -- runs of one route, stretches of same-switch pairs (one
+    entry each), pairs with no entries (row -1), random pairs and, on the
+    torus, DFS routes longer than a slot (the direct walk) -- written at
+    several phases of the entry array against the 128-B lines, by three
+    walker / storer shapes.  The u32 entries equal the int32 one-role
+    kernel's, and nothing outside the output range is written.  (Also the
+    parity test of the line-owned slots measured in round 6,
+    tools/diag/flows_line_owned.patch.)"""
+    import torch
+    fabric = T.by_name(fab)
+    csr = fabric.csr()
+    ctx.upload(csr)
+    dev = torch.device("cuda", 0)
+    hv, hp = fabric.host_table()
+    srcs = np.unique(hv).astype(np.int32)
+    H = len(hv)
+    order = np.argsort(hv, kind="stable")        # hosts grouped by switch
+    par, prt, hop = ctx.dfs_tables(srcs)
+    tp, tt, th = (torch.from_numpy(x).to(dev) for x in (par, prt, hop))
+    rng = np.random.default_rng(13)
+    A, B, R = [], [], []
+    for _ in range(600):
+        kind = int(rng.integers(0, 6))
+        if kind in (0, 5):                       # a run: one source, hosts of few switches
+            cnt = int(rng.integers(1, 60 if kind == 0 else 300))
+            b0 = int(rng.integers(0, H))
+            a = np.full(cnt, rng.integers(0, H))
+            b = order[(b0 + np.arange(cnt)) % H]
+        elif kind == 1:                          # same-switch pairs: one entry each
+            cnt = int(rng.integers(1, 45))
+            a = rng.integers(0, H, cnt)
+            b = a.copy()
+        elif kind == 2:                          # random pairs
+            cnt = int(rng.integers(1, 30))
+            a, b = rng.integers(0, H, cnt), rng.integers(0, H, cnt)
+        else:                                    # no entries (unknown row)
+            cnt = int(rng.integers(1, 20))
+            a, b = rng.integers(0, H, cnt), rng.integers(0, H, cnt)
+        A.append(a)
+        B.append(b)
+        R.append(np.full(cnt, kind == 3 or kind == 4))
+    a, b, none = np.concatenate(A), np.concatenate(B), np.concatenate(R)
+    rows = np.where(none, -1, np.searchsorted(srcs, hv[a])).astype(np.int32)
+    dsts = hv[b].astype(np.int32)
+    last = hp[b].astype(np.int32)
+    n = len(rows)
+    r, d, l = (torch.from_numpy(x).to(dev) for x in (rows, dsts, last))
+    off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    ctx.route_offsets_device(th.data_ptr(), r.data_ptr(), d.data_ptr(), n, off.data_ptr(),
+                             nrows=len(srcs))
+    ctx.synchronize()
+    tot = int(off[-1].item())
+    o = off.cpu().numpy()
+    assert (np.diff(o) == 0).sum() >= 100 and (np.diff(o) == 1).sum() >= 100
+    sw = torch.zeros(tot, dtype=torch.int32, device=dev)
+    pt = torch.zeros(tot, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    monkeypatch.setenv("SDNROUTE_ROUTE_PIPE", "0")
+    ctx.expand_routes_device(tp.data_ptr(), tt.data_ptr(), len(srcs), r.data_ptr(), d.data_ptr(),
+                             l.data_ptr(), n, off.data_ptr(), sw.data_ptr(), pt.data_ptr())
+    ctx.synchronize()
+    assert ctx.last_kernel() == "route_seg_packed_kernel<1024>"
+    want = (sw.cpu().numpy().astype(np.uint32) & 0xFFFF) | (pt.cpu().numpy().astype(np.uint32) << 16)
+    for shape in ("2,2,4", "1,1,4", "8,4,2"):
+        monkeypatch.setenv("SDNROUTE_ROUTE_PIPE", shape)
+        for phase in (0, 1, 7, 13, 31, 37):      # entries past a 128-B boundary
+            buf = torch.zeros(tot + 96, dtype=torch.int32, device=dev)
+            assert buf.data_ptr() % 128 == 0
+            torch.cuda.synchronize(dev)
+            ctx.expand_routes_packed_device(tp.data_ptr(), tt.data_ptr(), len(srcs), r.data_ptr(),
+                                            d.data_ptr(), l.data_ptr(), n, off.data_ptr(),
+                                            buf[phase:].data_ptr())
+            ctx.synchronize()
+            assert ctx.last_kernel() == "route_seg_pipe_kernel<u32>"
+            e = buf.cpu().numpy().view(np.uint32)
+            np.testing.assert_array_equal(e[phase:phase + tot], want, err_msg="%s %d" % (shape, phase))
+            assert not e[:phase].any() and not e[phase + tot:].any()
+
+
 @pytest.mark.parametrize("scan", ["fused", "4"])
 @pytest.mark.parametrize("npairs", [1, 8191, 8192, 8193, 3_000_000])
 def test_route_offsets_scan(ctx, monkeypatch, scan, npairs):

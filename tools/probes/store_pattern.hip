@@ -48,8 +48,9 @@ __global__ __launch_bounds__(256) void group_kernel(uint4 *o, size_t ngroups, in
 // `run` 4-B entries starting at arbitrary 4-B offsets; each run is stored
 // as the seg kernels do: up to 3 single entries to the 16-B boundary, 16-B
 // stores, up to 3 single entries at the end (RUNFLAT: the same group stored
-// as one range, head and tail once per group)
-template <bool RUNFLAT, bool NT = false, bool XCD = false>
+// as one range, head and tail once per group; LA: the head runs to the next
+// 128-B line instead, up to 31 entries)
+template <bool RUNFLAT, bool NT = false, bool XCD = false, bool LA = false, int FULL = 0>
 __global__ __launch_bounds__(256) void runs_kernel(uint32_t *o, size_t ngroups, int per_group,
                                                    int run)
 {
@@ -65,12 +66,19 @@ __global__ __launch_bounds__(256) void runs_kernel(uint32_t *o, size_t ngroups, 
         gend = (x + 1) * gx < ngroups ? (x + 1) * gx : ngroups;
     }
     for (size_t g = g0; g < gend; g += nwaves) {
-        const size_t gbase = g * (size_t)per_group + 1;      // groups start 4 B past a boundary
-        const int len = per_group - 2;
+        // groups start 4 B past a boundary and leave the line they share
+        // with the next group partly unwritten (FULL 1: whole lines, 144
+        // each; FULL 2: groups 4 B past a boundary that cover the buffer, so
+        // every line is written whole, the boundary line by two waves)
+        const size_t gbase = g * (size_t)per_group + (FULL == 1 ? 0 : 1);
+        const int len = per_group - (FULL ? 0 : 2);
         for (int r0 = 0; r0 < len; r0 += RUNFLAT ? len : run) {
             const int total = RUNFLAT ? len : min(run, len - r0);
             uint32_t *p = o + gbase + r0;
-            const int hd = min(total, (int)(((16u - ((uint32_t)(uintptr_t)p & 15u)) & 15u) >> 2));
+            // LA: single entries up to the next 128-B line, so that every
+            // wave of 16-B stores covers 8 whole lines (else to 16 B)
+            const uint32_t m = LA ? 127u : 15u;
+            const int hd = min(total, (int)((((m + 1u) - ((uint32_t)(uintptr_t)p & m)) & m) >> 2));
             if (lane < hd) p[lane] = (uint32_t)lane;
             const int bend = hd + ((total - hd) & ~3);
             for (int t0 = hd; t0 < bend; t0 += 256) {
@@ -107,7 +115,7 @@ int main()
     for (int rep = 0; rep < 3; ++rep) {
         // the real pattern: 18,432-B groups (64 pairs x 72 entries), runs of 1,728 entries
         const int pg = 4608, nr = (int)(bytes / 4 / pg);
-        for (int which = 0; which < 4; ++which) {
+        for (int which = 0; which < 9; ++which) {
             CK(hipEventRecord(a));
             if (which == 0)
                 hipLaunchKernelGGL(runs_kernel<false>, dim3(cus * 8), dim3(256), 0, 0,
@@ -118,15 +126,32 @@ int main()
             else if (which == 2)
                 hipLaunchKernelGGL((runs_kernel<false, true>), dim3(cus * 8), dim3(256), 0, 0,
                                    reinterpret_cast<uint32_t *>(o), (size_t)nr - 1, pg, 1728);
-            else
+            else if (which == 3)
                 hipLaunchKernelGGL((runs_kernel<false, false, true>), dim3(cus * 8), dim3(256), 0, 0,
+                                   reinterpret_cast<uint32_t *>(o), (size_t)nr - 1, pg, 1728);
+            else if (which == 4)
+                hipLaunchKernelGGL((runs_kernel<false, false, false, true>), dim3(cus * 8), dim3(256), 0, 0,
+                                   reinterpret_cast<uint32_t *>(o), (size_t)nr - 1, pg, 1728);
+            else if (which == 5)
+                hipLaunchKernelGGL((runs_kernel<false, false, false, true, 1>), dim3(cus * 8), dim3(256), 0, 0,
+                                   reinterpret_cast<uint32_t *>(o), (size_t)nr - 1, pg, 1728);
+            else if (which == 6)
+                hipLaunchKernelGGL((runs_kernel<true, false, false, true, 1>), dim3(cus * 8), dim3(256), 0, 0,
+                                   reinterpret_cast<uint32_t *>(o), (size_t)nr - 1, pg, 1728);
+            else if (which == 7)
+                hipLaunchKernelGGL((runs_kernel<false, false, false, true, 2>), dim3(cus * 8), dim3(256), 0, 0,
+                                   reinterpret_cast<uint32_t *>(o), (size_t)nr - 1, pg, 1728);
+            else
+                hipLaunchKernelGGL((runs_kernel<false, false, true, true, 2>), dim3(cus * 8), dim3(256), 0, 0,
                                    reinterpret_cast<uint32_t *>(o), (size_t)nr - 1, pg, 1728);
             CK(hipEventRecord(b));
             CK(hipEventSynchronize(b));
             float ms = 0;
             CK(hipEventElapsedTime(&ms, a, b));
-            const double wb = (double)(nr - 1) * (pg - 2) * 4.0;
-            printf("%-10s %.3f ms  %.2f TB/s\n", which == 0 ? "runs" : which == 1 ? "runs-flat" : which == 2 ? "runs-nt" : "runs-xcd", ms,
+            const double wb = (double)(nr - 1) * (pg - (which >= 5 ? 0 : 2)) * 4.0;
+            printf("%-10s %.3f ms  %.2f TB/s\n", which == 0 ? "runs" : which == 1 ? "runs-flat" : which == 2 ? "runs-nt" :
+                   which == 3 ? "runs-xcd" : which == 4 ? "runs-line" : which == 5 ? "line-full" :
+                   which == 6 ? "flat-full" : which == 7 ? "shared" : "shared-xcd", ms,
                    wb / (ms * 1e-3) / 1e12);
         }
         for (int which = 0; which < 4; ++which) {
