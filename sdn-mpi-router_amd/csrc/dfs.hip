@@ -1715,6 +1715,13 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
 #ifndef SDNR_ASYNC_G
 #define SDNR_ASYNC_G 8
 #endif
+// table flush: vertices per thread per pass (one pass for k=48's 2,880
+// switches at 8 waves: 1 / 144 sources 45.4 / 47.1 -> 43.7 / 45.1 us; 12
+// gained 1 % more there but cost the dragonfly's compact kernel registers:
+// 2,064 sources 169 -> 217 us; profiles/r06_flush_ab)
+#ifndef SDNR_ASYNC_FLUSH_U
+#define SDNR_ASYNC_FLUSH_U 6
+#endif
 #ifndef SDNR_ASYNC_G_DW
 #define SDNR_ASYNC_G_DW 16
 #endif
@@ -2151,12 +2158,17 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
         SDNR_STAMP(ph2);
 #endif
 
-        // tables: U vertices per thread, their port loads (one ELL load, or
-        // row_ptr + port) all in flight before the stores
-        for (int v0 = threadIdx.x; v0 < V; v0 += U * blockDim.x) {
-            int p[U], sl[U], pt[U];
+        // tables: UF vertices per thread, their port loads (one ELL load, or
+        // row_ptr + port) all in flight before the stores.  A wave's
+        // vector-memory counter retires loads and stores in issue order, so
+        // a port gather issued after the previous pass's table stores waits
+        // for their acknowledgement: fewer, wider passes (k=48 at 8 waves:
+        // one pass)
+        constexpr int UF = SDNR_ASYNC_FLUSH_U;
+        for (int v0 = threadIdx.x; v0 < V; v0 += UF * blockDim.x) {
+            int p[UF], sl[UF], pt[UF];
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
+            for (int k = 0; k < UF; ++k) {
                 const int v = v0 + k * (int)blockDim.x;
                 p[k] = -1;
                 sl[k] = -1;
@@ -2172,13 +2184,13 @@ __global__ __launch_bounds__(NW * 64, C16 ? 7 : 1) void dfs_async_kernel(
                 }
             }
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
+            for (int k = 0; k < UF; ++k) {
                 pt[k] = -1;
                 if (sl[k] >= 0)
                     pt[k] = W > 0 ? ell_port[(size_t)p[k] * W + sl[k]] : port[row_ptr[p[k]] + sl[k]];
             }
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
+            for (int k = 0; k < UF; ++k) {
                 const int v = v0 + k * (int)blockDim.x;
                 if (v < V) {
                     if (PACKED) {                // parent | port << 16, -1 -> 0xFFFF
