@@ -1261,3 +1261,25 @@ def test_route_offsets_scan(ctx, monkeypatch, scan, npairs):
                              nrows=V)
     ctx.synchronize()
     np.testing.assert_array_equal(off.cpu().numpy(), want)
+
+
+def test_empty_batches(ctx):
+    """Zero sources, destinations and pairs through every batch entry point:
+    empty results and no error (the C ABI returns SDNR_OK and launches
+    nothing; the offsets of zero pairs are [0])."""
+    csr = T.fat_tree(8).csr()
+    ctx.upload(csr)
+    V = csr.V
+    e = np.empty(0, np.int32)
+    p, t, h = ctx.dfs_tables(e)
+    assert p.shape == t.shape == h.shape == (0, V)
+    assert ctx.dfs_tables_packed(e).shape == (0, V)
+    assert ctx.dfs_tables_slots(e).shape == (0, V)
+    d, nh, nhp = ctx.shortest_tables(e)
+    assert d.shape == nh.shape == nhp.shape == (0, V)
+    assert ctx.ecmp_counts(np.empty((0, V), np.uint16)).shape == (0, V)
+    par, prt, hop = ctx.dfs_tables(np.array([0, 1], np.int32))
+    off, sw, hp = ctx.expand_routes(par, prt, hop, e, e, e)
+    assert off.tolist() == [0] and sw.size == 0 and hp.size == 0
+    # and one source still computes afterwards
+    np.testing.assert_array_equal(ctx.dfs_tables(np.array([1], np.int32))[0], par[1:2])

@@ -740,3 +740,23 @@ def test_route_entries_wide_host_port(monkeypatch):
     narrow = [(a, b) for a, b in pairs if b != wide]
     assert db.find_routes(narrow) == [O.find_route_pair(db, a, b) for a, b in narrow]
     assert db.engine.ctx.last_kernel() == "route_seg_packed_kernel<1024,u32>"
+
+
+@pytest.mark.gpu
+def test_dropin_empty_batches():
+    """The batch calls of the drop-in on an empty request list: empty
+    results, as the reference's loop over no pairs installs nothing."""
+    g = G.Golden("fat_tree_k8")
+    db = g.fabric().populate(TopologyDB())
+    assert db.find_routes([]) == []
+    assert db.find_routes([], multiple=True) == []
+    off, dp, pt = db.route_entries([])
+    assert list(off) == [0] and len(dp) == 0 and len(pt) == 0
+    dpids, soff, pid, opt, last = db.switch_fdb_entries([])
+    assert len(dpids) == len(pid) == len(opt) == len(last) == 0 and list(soff) == [0]
+    dpids, soff, sr, dr, opt, last = db.mpi_flow_entries({})
+    assert len(dpids) == len(sr) == len(dr) == len(opt) == 0 and list(soff) == [0]
+    dpids, soff, sr, dr, opt, last = db.mpi_flow_entries({0: g.fabric().host_macs()[0]})
+    assert len(dpids) == 0 and list(soff) == [0]          # one rank: no pairs
+    macs = g.fabric().host_macs()
+    assert db.find_routes([(macs[0], macs[1])]) == [db.find_route(macs[0], macs[1])]
