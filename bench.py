@@ -1343,6 +1343,12 @@ def main():
             "compulsory_bytes": compulsory,
             "compulsory_gbs": compulsory / (kern_ms / 1e3) / 1e9,
             **_measured(traffic, kern_ms),
+            **({"note": "bytes_per_launch counts SURVEY.md 8(d)'s algorithmic bytes (the CSR "
+                        "once per destination); the plane BFS reads it once per 64 "
+                        "destinations (one bit each), so frac is an effective rate and can "
+                        "pass 1; hbm_frac is the PMC-measured HBM fraction"}
+               if args.mode == "shortest" and ctx.last_kernel().startswith("msbfs_plane")
+               else {}),
         },
         "switch_pair_routes_per_s": float(S) * V / (ms_per_step / 1e3),
         "teps": float(hi - lo) * E / (kern_ms / 1e3),
