@@ -87,11 +87,12 @@ def parse():
                     help="dfs mode: skip the materialised flow-entry rate of every host pair")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0,
                     help="bound on the CPU baseline's work")
-    ap.add_argument("--assemble", choices=["all", "root"], default="root",
+    ap.add_argument("--assemble", choices=["all", "root", "none"], default="root",
                     help="N > 1: tables assembled on rank 0, the controller's GPU (RCCL "
                          "point-to-point receives into the root, default), or on every "
                          "rank (RCCL all-gather); the other form is measured beside it in "
-                         "the multi_gpu block")
+                         "the multi_gpu block.  none: each rank keeps its shard (the "
+                         "line's own fallback when neither form passes the preflight)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="steps kept in flight on their own streams (0: auto -- 3 at N > 1 "
                          "when one rank's share is under 4 sources per CU and leaves most of "
@@ -733,11 +734,13 @@ def multi_gpu_extras(args, world, rank, local, dev, csr, srcs, per, packed, slot
              else D.gather_rows_to_root(t, g)).wait()
 
     kmax, kmin = _max_min(kern_ms, dev)
-    gather_ms = timed(gather_only)
+    gather_ms = timed(gather_only) if args.assemble != "none" else 0.0
     other = "root" if args.assemble == "all" else "all"
     # the secondary form is reported, never fatal for the headline (a form
     # that failed its preflight is not run at all)
     try:
+        if args.assemble == "none":
+            raise RuntimeError("no assembly: the shards stay on their ranks")
         if check and check.get(other) != "ok":
             raise RuntimeError("preflight: %s" % check.get(other))
         assemble[0] = other
@@ -798,6 +801,18 @@ def multi_gpu_extras(args, world, rank, local, dev, csr, srcs, per, packed, slot
     return res
 
 
+def pick_assembly(requested, check):
+    """The assembly form an N > 1 line runs, from the preflight's verdicts
+    (distributed.check_assembly): the requested form if it passed, else the
+    other RCCL form if that passed, else none (each rank keeps its shard).
+    Returns (form, "requested -> form" or None)."""
+    if requested == "none" or check.get(requested) == "ok":
+        return requested, None
+    other = "all" if requested == "root" else "root"
+    form = other if check.get(other) == "ok" else "none"
+    return form, "%s -> %s" % (requested, form)
+
+
 # why the line's default assembly is what it is (printed in config)
 ASSEMBLE_REASON = {
     "root": "tables assembled on rank 0, the controller's GPU (the one process that serves "
@@ -809,6 +824,9 @@ ASSEMBLE_REASON = {
     "all": "tables assembled on every rank by one RCCL all-gather per table over xGMI (the "
            "north_star's form); the root-only point-to-point form is timed beside it "
            "(multi_gpu.assemble_root)",
+    "none": "each rank keeps its shard of the tables (sources partitioned, no data-path "
+            "collective): chosen by --assemble none, or by the line itself when neither "
+            "RCCL assembly form passed the preflight (multi_gpu.assembly_check)",
 }
 
 
@@ -914,7 +932,14 @@ def main_rehearse(args, world, rank):
     out = torch.empty((world * per, 1), dtype=torch.int32)
     routes = float(len(srcs)) * fabric.n_hosts
 
+    args.assemble, fb = pick_assembly(args.assemble, check)
+    if fb:
+        check["fallback"] = fb
+
     def step():                             # the "step": this rank's ids assembled
+        if args.assemble == "none":         # each rank keeps its shard
+            out[rank * per:(rank + 1) * per].copy_(mine)
+            return
         (D.all_gather_rows_async(mine, out) if args.assemble == "all"
          else D.gather_rows_to_root(mine, out)).wait()
 
@@ -942,7 +967,10 @@ def main_rehearse(args, world, rank):
                                "value": routes / (b / 1e3)}}
     shards = [None] * world
     dist.all_gather_object(shards, (rank, lo, hi, os.getpid()))
-    if args.assemble == "root":
+    if args.assemble == "none":             # this rank's own slice holds its shard
+        ok = bool(np.array_equal(out[rank * per:(rank + 1) * per].view(-1).numpy(),
+                                 mine.view(-1).numpy()))
+    elif args.assemble == "root":
         ok = rank != 0 or bool(np.array_equal(D.unpad(out.view(-1), len(srcs)).numpy(), srcs))
     else:
         ok = bool(np.array_equal(D.unpad(out.view(-1), len(srcs)).numpy(), srcs))
@@ -1062,10 +1090,9 @@ def main():
         # form that raises or assembles wrong rows is reported, and the
         # headline falls back to the other one instead of losing the line
         assembly_check = D.check_assembly(dev)
-        other = "all" if args.assemble == "root" else "root"
-        if assembly_check.get(args.assemble) != "ok" and assembly_check.get(other) == "ok":
-            assembly_check["fallback"] = "%s -> %s" % (args.assemble, other)
-            args.assemble = other
+        args.assemble, fb = pick_assembly(args.assemble, assembly_check)
+        if fb:                              # the line is kept either way
+            assembly_check["fallback"] = fb
     if args.mode == "flows":
         return main_flows(args, world, rank, local, dev)
     if args.mode == "ecmp":
@@ -1177,7 +1204,7 @@ def main():
                                           tb[1].data_ptr(), tb[2].data_ptr())
             if ev is not None:
                 ev[1].record(st)
-            if world > 1:                   # assemble [sources][V] on every rank / rank 0
+            if world > 1 and assemble[0] != "none":   # [sources][V] on every rank / rank 0
                 for t, g in zip(tb, gathered[k]):
                     pending[k].append(D.all_gather_rows_async(t, g) if assemble[0] == "all"
                                       else D.gather_rows_to_root(t, g))
@@ -1330,7 +1357,9 @@ def main():
                 world, (" + tables assembled %s over RCCL (double-buffered: step i+1's "
                         "kernel overlaps step i's assembly)" % (
                             "on every rank by all-gather" if args.assemble == "all"
-                            else "on rank 0 by point-to-point receives")) if world > 1 else ""),
+                            else "on rank 0 by point-to-point receives"))
+                       if world > 1 and args.assemble != "none" else
+                       (" (each rank keeps its shard: no assembly)" if world > 1 else "")),
             "steps_in_flight": inflight,
         },
         "roofline": {

@@ -30,7 +30,7 @@ def _run(args, env, timeout=300):
                           env=env, capture_output=True, text=True, timeout=timeout)
 
 
-@pytest.mark.parametrize("n,form", [(2, "root"), (3, "root"), (2, "all")])
+@pytest.mark.parametrize("n,form", [(2, "root"), (3, "root"), (2, "all"), (2, "none")])
 def test_bench_gpus_n_launches_n_ranks(n, form):
     r = _run(["--gpus", str(n), "--rehearse", "--steps", "2", "--assemble", form,
               "--cpu-budget-s", "2"], _env())
@@ -45,7 +45,7 @@ def test_bench_gpus_n_launches_n_ranks(n, form):
     # contiguous shards covering every k=48 host-bearing switch once
     assert line["shards"][0]["lo"] == 0 and line["shards"][-1]["hi"] == 1152
     assert all(a["hi"] == b["lo"] for a, b in zip(line["shards"], line["shards"][1:]))
-    assert line["sources_assembled_exactly"] is True
+    assert line["sources_assembled_exactly"] is True     # (none: each rank's own shard)
     # the N > 1 line's honesty keys: one step's latency, the
     # rate by steps in flight, both assembly forms preflighted, the scaling
     # efficiency against the same run's N = 1 base, why this assembly, and
@@ -75,3 +75,22 @@ def test_bench_refuses_more_gpus_than_visible():
     r = _run(["--gpus", "1"], _env(), timeout=120)
     assert r.returncode != 0
     assert "GPU(s) are visible" in r.stderr
+
+
+def test_pick_assembly_fallbacks():
+    """The N > 1 line's assembly after the preflight: the requested form when
+    it passed, the other RCCL form when only that passed, no assembly (each
+    rank keeps its shard) when neither did -- the line is never lost."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    ok, bad = "ok", "error: RuntimeError('x')"
+    assert b.pick_assembly("root", {"root": ok, "all": ok}) == ("root", None)
+    assert b.pick_assembly("all", {"root": ok, "all": ok}) == ("all", None)
+    assert b.pick_assembly("root", {"root": bad, "all": ok}) == ("all", "root -> all")
+    assert b.pick_assembly("all", {"root": ok, "all": "wrong rows assembled"}) == ("root", "all -> root")
+    assert b.pick_assembly("root", {"root": bad, "all": bad}) == ("none", "root -> none")
+    assert b.pick_assembly("none", {"root": bad, "all": bad}) == ("none", None)
+    for form in ("root", "all", "none"):
+        assert b.ASSEMBLE_REASON[form]

@@ -2,10 +2,12 @@
 # round 6: the N > 1 bench path as 2 gloo ranks on one GPU (BENCH_DEVICE=0;
 # RCCL refuses two ranks on one device), both assembly forms and the
 # shortest mode; every key of the N > 1 line is produced, the values are
-# meaningless (gloo moves the tables through host memory)
+# meaningless (gloo moves the tables through host memory).  Usage:
+# bash tools/r6_rehearse.sh ["MODE ASSEMBLE" ...]
 set -u
 O=gpurun_out/r6_multi; mkdir -p $O
-for spec in "dfs root" "dfs all" "shortest root"; do
+[ $# -eq 0 ] && set -- "dfs root" "dfs all" "shortest root"
+for spec in "$@"; do
   set -- $spec
   BENCH_DEVICE=0 BENCH_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
     --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 \
